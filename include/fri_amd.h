@@ -1,0 +1,175 @@
+/*
+ * fri_amd.h — C ABI of the MI355X-native FRI commit path (libfri_amd.so).
+ *
+ * Drop-in boundary for the reference crate `stark-101`
+ * (RazorClient/Stark-prover).  Each entry point names the reference function
+ * it replaces (path:line in the reference tree).  Plain pointers and sizes
+ * only; no torch / HIP types in any signature.
+ *
+ * Field: p = 3*2^30 + 1 = 3221225473, generator g = 5 (frozen spec,
+ * SURVEY.md §8).  Field elements cross the boundary as canonical uint32_t
+ * (value < p) — the reference's FieldElement<M>{value: u64} is not repr(C),
+ * so the Rust shim copies `.value() as u32`.
+ *
+ * Host buffers are caller-owned and only borrowed for the duration of a call.
+ * Device memory, streams and graphs are owned by the fri_ctx.  A context is
+ * not re-entrant: use one per host thread.  Every call returns FRI_OK (0) or
+ * a FRI_E* code; fri_last_error() describes the last failure on the context.
+ * The reference panics where these return an error (ops.rs:143,
+ * interpolation.rs:127, merkle/mod.rs:25, channel.rs:65); the Rust shim maps
+ * non-zero codes back to panic!().
+ */
+#ifndef FRI_AMD_H
+#define FRI_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FRI_P          3221225473u   /* 3*2^30 + 1 */
+#define FRI_GENERATOR  5u
+#define FRI_MAX_ROUNDS 32
+#define FRI_MAX_LAYERS (FRI_MAX_ROUNDS + 1)
+
+enum {
+    FRI_OK      = 0,
+    FRI_EINVAL  = 1,   /* bad argument (sizes, d > n, value >= p, ...)      */
+    FRI_ENOMEM  = 2,   /* device or host allocation failed                  */
+    FRI_EHIP    = 3,   /* HIP runtime error                                 */
+    FRI_ENODEV  = 4,   /* no usable gfx950 device                           */
+    FRI_ERCCL   = 5,   /* collective failure (multi-GPU)                    */
+    FRI_ESTATE  = 6,   /* call out of order (e.g. no committed layers)      */
+    FRI_EDEGREE = 7    /* polynomial degree too large for the domain: the
+                          reference would exhaust the domain and panic in
+                          MerkleTree::root() (merkle/mod.rs:25)             */
+};
+
+/* Fiat-Shamir transcript state — src/channel/channel.rs:14-20.
+ * The reference keeps `state: String` = "" or the 64-char lowercase hex of
+ * a SHA-256 digest; here it is the 32 raw digest bytes + has_state flag. */
+typedef struct {
+    uint8_t  digest[32];
+    uint32_t has_state;   /* 0 => state == "" (Channel::new, channel.rs:24-30) */
+} fri_channel_state;
+
+/* Result of fri_commit — the transcript-visible part of FRIProof
+ * (src/fri/fri_commit.rs:9-13) plus the channel messages it produced.
+ * Layer evaluations and Merkle levels stay on the device and are read back
+ * on demand with fri_layer_copy / fri_tree_level_copy. */
+typedef struct {
+    uint32_t n_layers;                       /* R+1 committed layers          */
+    uint32_t n_rounds;                       /* R folds (= betas drawn)       */
+    uint32_t log_n;                          /* layer k has 2^(log_n-k) elems */
+    uint32_t final_value;                    /* fri_commit.rs:109-113         */
+    int32_t  final_degree;                   /* 0, or -1 for the zero poly    */
+    uint32_t reserved;
+    uint8_t  roots[FRI_MAX_LAYERS][32];      /* Merkle root bytes per layer   */
+    uint32_t betas[FRI_MAX_ROUNDS];          /* beta_k, canonical             */
+    fri_channel_state channel_out;           /* channel state after the final send */
+} fri_commit_result;
+
+typedef struct fri_ctx fri_ctx;
+
+/* flags for fri_commit* */
+#define FRI_FLAG_FORCE_BETAS 1u   /* test hook: use forced_betas[k] instead of the
+                                     channel's draw (transcript still absorbs roots) */
+#define FRI_FLAG_NO_GRAPH    2u   /* run eagerly instead of replaying a hipGraph   */
+
+/* ---------------------------------------------------------------- context */
+/* Opens `device` (HIP ordinal) and sizes scratch for codewords up to
+ * 2^log_n_max.  Returns FRI_ENODEV when no gfx950 device is present. */
+int         fri_ctx_create(int device, uint32_t log_n_max, fri_ctx** out);
+int         fri_ctx_destroy(fri_ctx* ctx);
+const char* fri_last_error(const fri_ctx* ctx);    /* never NULL; "" if none */
+const char* fri_version(void);
+
+/* ------------------------------------------------------- field / batch ops */
+/* Batch inverse with inverse(0) = 0 — same results as element-wise
+ * FieldElement::inverse (src/fields/element.rs:54-57, Fermat a^(p-2)). */
+int fri_batch_inverse(fri_ctx* ctx, const uint32_t* in, uint32_t* out, size_t n);
+
+/* ------------------------------------------------------ polynomial layer */
+/* Low-degree extension: evals[i] = P(offset * w_n^i), i < n = 2^log_n,
+ * P given by d <= n coefficients (coefficient j = x^j).  Replaces
+ * `domain.map(|x| poly.evaluate(x))` (src/fri/fri_commit.rs:78,
+ * src/polynomial/ops.rs:76-83) on the coset domain of
+ * src/fri/coset_fri.rs:32-36.  offset = 1 gives the plain subgroup. */
+int fri_lde(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n,
+            uint32_t offset, uint32_t* evals_out);
+
+/* Interpolation on the same coset: the unique P, deg P < n, with
+ * P(offset*w_n^i) = ys[i].  Replaces Polynomial::interpolate
+ * (src/polynomial/ops.rs:239-241 -> interpolation.rs:121-152) for coset
+ * domains.  coeffs_out holds n entries; *len_out = trimmed length
+ * (Polynomial::new semantics, ops.rs:19-37). */
+int fri_interpolate(fri_ctx* ctx, const uint32_t* ys, uint32_t log_n, uint32_t offset,
+                    uint32_t* coeffs_out, size_t* len_out);
+
+/* Evaluation of P (d coefficients) at `count` arbitrary points
+ * (src/polynomial/ops.rs:76-83, Horner semantics). */
+int fri_evaluate(fri_ctx* ctx, const uint32_t* coeffs, size_t d, const uint32_t* xs,
+                 size_t count, uint32_t* out);
+
+/* ---------------------------------------------------------------- FRI ops */
+/* One FRI fold of a layer of size m = 2^log_m living on the coset
+ * layer_offset * <w_m> (natural order): out[i] = P'(x_i^2), i < m/2, with
+ * P' = even(P) + beta*odd(P).  Bit-identical to next_fri_layer's
+ * coefficient fold + re-evaluation (src/fri/fri_commit.rs:53-65). */
+int fri_fold(fri_ctx* ctx, const uint32_t* layer, uint32_t log_m, uint32_t layer_offset,
+             uint32_t beta, uint32_t* out);
+
+/* Merkle root of n field elements: MerkleTree::new(values).root()
+ * (src/merkle/mod.rs:10-26 over rs_merkle 1.4.2, SHA-256, leaf =
+ * SHA256(u64 big-endian)).  root32 = raw digest bytes; the reference's
+ * `root() -> String` is their lowercase hex.  n must be >= 1. */
+int fri_merkle_root(fri_ctx* ctx, const uint32_t* values, size_t n, uint8_t root32[32]);
+
+/* ---------------------------------------------------------- FRI commit */
+/* Full FRI commit — fri_commit(poly, domain, &mut channel)
+ * (src/fri/fri_commit.rs:72-122): LDE of `coeffs` on offset*<w_n>,
+ * n = 2^log_n; per layer SHA-256 Merkle tree, channel.send(root_hex),
+ * beta = channel.receive_random_field_element(), fold; loop while the
+ * folded polynomial's degree >= 1; channel.send(final.to_bytes()).
+ * chan_in may be NULL (fresh Channel::new()).  Layers and trees stay on the
+ * device until the next commit on this context. */
+int fri_commit(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n,
+               uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+               const uint32_t* forced_betas, fri_commit_result* out);
+
+/* Same, with the coefficients already resident in device memory
+ * (d_coeffs: a device pointer; may be fri_ctx_input_buffer()). */
+int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
+                      uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                      const uint32_t* forced_betas, fri_commit_result* out);
+
+/* Device buffer of >= d words owned by the context that fri_commit_device
+ * reads without a copy.  Valid until fri_ctx_destroy. */
+int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
+
+/* Read-back of the last commit (FRIProof::fri_layers / fri_merkles). */
+int fri_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out, size_t cap);
+/* Merkle level `level` (0 = leaf hashes) of layer `layer`, as 32-byte digests. */
+int fri_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level, uint8_t* out, size_t cap);
+
+/* Decommitment helper (src/fri/fri_commit.rs:137-165): value and the
+ * rs_merkle authentication path (sibling hashes leaf->root) of `index` in
+ * committed layer `layer`.  path must hold 32*depth bytes; *depth_out set. */
+int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint32_t* value_out,
+                  uint8_t* path, uint32_t* depth_out);
+
+/* ------------------------------------------------------------ diagnostics */
+/* Per-kernel-class device time (ms) accumulated while profiling is enabled
+ * (hipEvents recorded on the context's stream around each launch class).
+ * names: "lde", "merkle_leaf", "merkle_node", "fold", "coeff_fold", "channel". */
+int fri_set_profiling(fri_ctx* ctx, int enabled);
+int fri_get_profile(fri_ctx* ctx, const char* kernel_class, double* total_ms, uint64_t* launches,
+                    uint64_t* bytes);
+int fri_reset_profile(fri_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FRI_AMD_H */

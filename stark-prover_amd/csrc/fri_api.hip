@@ -1,0 +1,644 @@
+// fri_api.hip — context, commit plan (static launch sequence + hipGraph) and
+// the extern "C" entry points declared in include/fri_amd.h.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/fri_amd.h"
+#include "fri_internal.hpp"
+#include "sha256.hpp"
+
+using namespace fri;
+
+static_assert(MAXR == FRI_MAX_ROUNDS, "round bound");
+
+namespace {
+
+struct ProfEntry { double ms = 0; uint64_t launches = 0; uint64_t bytes = 0; };
+
+struct Plan {
+    bool valid = false;
+    uint32_t log_n = 0;
+    size_t d = 0;
+    uint32_t offset = 0;
+    int rmax = 0;
+    uint32_t* d_in = nullptr;   size_t in_cap = 0;
+    uint32_t* coefA = nullptr;
+    uint32_t* coefB = nullptr;  size_t coef_cap = 0;
+    uint32_t* layers = nullptr; size_t layer_off[MAXR + 2] = {0};
+    uint32_t* trees = nullptr;  size_t tree_off[MAXR + 2] = {0};
+    uint32_t* xinv = nullptr;   size_t xinv_off[MAXR + 2] = {0};
+    uint32_t* pre_lo = nullptr;
+    uint32_t* pre_hi = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    bool graph_profiled = false;
+};
+
+// One timed launch group: events recorded around it on the context stream.
+struct TimedSpan { std::string cls; hipEvent_t b, e; uint64_t bytes; };
+
+}  // namespace
+
+struct fri_ctx {
+    int device = 0;
+    uint32_t log_n_max = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    uint32_t* tw_fwd = nullptr;     // Montgomery w^j, j < 2^(log_n_max-1)
+    uint32_t* tw_inv = nullptr;
+    uint32_t* scratch_a = nullptr;  // 2^log_n_max words each
+    uint32_t* scratch_b = nullptr;
+    uint32_t* scratch_c = nullptr;
+    uint32_t* pow_lo = nullptr;
+    uint32_t* pow_hi = nullptr;
+    DevState* d_state = nullptr;
+    DevState* h_state = nullptr;    // pinned
+    Plan plan;
+    bool profiling = false;
+    std::map<std::string, ProfEntry> prof;
+    std::vector<TimedSpan> spans;      // recorded spans of the current commit
+    std::vector<hipEvent_t> event_pool;
+    size_t event_next = 0;
+};
+
+#define FRI_HIP(ctx, expr)                                                              \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess) {                                                         \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(_e);             \
+            return FRI_EHIP;                                                            \
+        }                                                                               \
+    } while (0)
+
+static int fail(fri_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+static bool check_canonical(const uint32_t* v, size_t n) {
+    for (size_t i = 0; i < n; i++)
+        if (v[i] >= P) return false;
+    return true;
+}
+
+static hipEvent_t pool_event(fri_ctx* ctx) {
+    if (ctx->event_next == ctx->event_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        ctx->event_pool.push_back(e);
+    }
+    return ctx->event_pool[ctx->event_next++];
+}
+
+// Record the begin of a timed span (only while profiling).
+static size_t span_begin(fri_ctx* ctx, const char* cls, uint64_t bytes) {
+    if (!ctx->profiling) return (size_t)-1;
+    TimedSpan sp{cls, pool_event(ctx), pool_event(ctx), bytes};
+    hipEventRecord(sp.b, ctx->stream);
+    ctx->spans.push_back(sp);
+    return ctx->spans.size() - 1;
+}
+static void span_end(fri_ctx* ctx, size_t id) {
+    if (id == (size_t)-1) return;
+    hipEventRecord(ctx->spans[id].e, ctx->stream);
+}
+static void spans_collect(fri_ctx* ctx) {
+    for (auto& sp : ctx->spans) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, sp.b, sp.e) == hipSuccess) {
+            auto& pe = ctx->prof[sp.cls];
+            pe.ms += ms;
+            pe.launches += 1;
+            pe.bytes += sp.bytes;
+        }
+    }
+    ctx->spans.clear();
+    ctx->event_next = 0;
+}
+
+// ------------------------------------------------------------ context ----
+extern "C" int fri_ctx_create(int device, uint32_t log_n_max, fri_ctx** out) {
+    if (!out) return FRI_EINVAL;
+    *out = nullptr;
+    if (log_n_max < 1 || log_n_max > 30) return FRI_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return FRI_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FRI_ENODEV;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return FRI_ENODEV;
+    fri_ctx* ctx = new fri_ctx();
+    ctx->device = device;
+    ctx->log_n_max = log_n_max;
+    const size_t N = (size_t)1 << log_n_max;
+    const size_t nhi = log_n_max > POW_LO_LOG ? ((size_t)1 << (log_n_max - POW_LO_LOG)) : 1;
+#define CK(expr)                                                    \
+    if ((expr) != hipSuccess) { fri_ctx_destroy(ctx); return FRI_ENOMEM; }
+    CK(hipSetDevice(device));
+    CK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    CK(hipMalloc(&ctx->tw_fwd, (N / 2 + 1) * 4));
+    CK(hipMalloc(&ctx->tw_inv, (N / 2 + 1) * 4));
+    CK(hipMalloc(&ctx->scratch_a, N * 4));
+    CK(hipMalloc(&ctx->scratch_b, N * 4));
+    CK(hipMalloc(&ctx->scratch_c, N * 4));
+    CK(hipMalloc(&ctx->pow_lo, ((size_t)1 << POW_LO_LOG) * 4));
+    CK(hipMalloc(&ctx->pow_hi, nhi * 4));
+    CK(hipMalloc(&ctx->d_state, sizeof(DevState)));
+    CK(hipHostMalloc(&ctx->h_state, sizeof(DevState), hipHostMallocDefault));
+#undef CK
+    launch_twiddles(ctx->tw_fwd, log_n_max, false, ctx->stream);
+    launch_twiddles(ctx->tw_inv, log_n_max, true, ctx->stream);
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) { fri_ctx_destroy(ctx); return FRI_EHIP; }
+    *out = ctx;
+    return FRI_OK;
+}
+
+static void plan_free(fri_ctx* ctx) {
+    Plan& p = ctx->plan;
+    if (p.exec) hipGraphExecDestroy(p.exec);
+    if (p.graph) hipGraphDestroy(p.graph);
+    hipFree(p.d_in); hipFree(p.coefA); hipFree(p.coefB); hipFree(p.layers);
+    hipFree(p.trees); hipFree(p.xinv); hipFree(p.pre_lo); hipFree(p.pre_hi);
+    p = Plan();
+}
+
+extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
+    if (!ctx) return FRI_EINVAL;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    plan_free(ctx);
+    for (auto e : ctx->event_pool) hipEventDestroy(e);
+    hipFree(ctx->tw_fwd); hipFree(ctx->tw_inv);
+    hipFree(ctx->scratch_a); hipFree(ctx->scratch_b); hipFree(ctx->scratch_c);
+    hipFree(ctx->pow_lo); hipFree(ctx->pow_hi);
+    hipFree(ctx->d_state);
+    if (ctx->h_state) hipHostFree(ctx->h_state);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return FRI_OK;
+}
+
+extern "C" const char* fri_last_error(const fri_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+extern "C" const char* fri_version(void) { return "fri_amd 0.1 (gfx950, p=3*2^30+1)"; }
+
+// ------------------------------------------------------- kernel-level ----
+extern "C" int fri_batch_inverse(fri_ctx* ctx, const uint32_t* in, uint32_t* out, size_t n) {
+    if (!ctx || (!in && n) || (!out && n)) return fail(ctx, FRI_EINVAL, "null argument");
+    if (!check_canonical(in, n)) return fail(ctx, FRI_EINVAL, "input not canonical (>= p)");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t cap = (size_t)1 << ctx->log_n_max;
+    for (size_t off = 0; off < n; off += cap) {
+        size_t m = n - off < cap ? n - off : cap;
+        FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, in + off, m * 4, hipMemcpyHostToDevice, ctx->stream));
+        launch_batch_inverse(ctx->scratch_a, ctx->scratch_b, m, 0, ctx->stream);
+        FRI_HIP(ctx, hipGetLastError());
+        FRI_HIP(ctx, hipMemcpyAsync(out + off, ctx->scratch_b, m * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return FRI_OK;
+}
+
+static NttPlan lde_plan(fri_ctx* ctx, uint32_t log_n) {
+    NttPlan p{};
+    p.log_n = log_n;
+    p.tw = ctx->tw_fwd;
+    p.log_tw = ctx->log_n_max;
+    return p;
+}
+
+extern "C" int fri_lde(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n, uint32_t offset,
+                       uint32_t* evals_out) {
+    if (!ctx || !evals_out || (d && !coeffs)) return fail(ctx, FRI_EINVAL, "null argument");
+    if (log_n > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n exceeds context capacity");
+    const size_t n = (size_t)1 << log_n;
+    if (d > n) return fail(ctx, FRI_EINVAL, "more coefficients than domain points");
+    if (offset == 0 || offset >= P) return fail(ctx, FRI_EINVAL, "offset must be a nonzero canonical element");
+    if (!check_canonical(coeffs, d)) return fail(ctx, FRI_EINVAL, "coefficient not canonical (>= p)");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    if (d) FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, coeffs, d * 4, hipMemcpyHostToDevice, ctx->stream));
+    NttPlan p = lde_plan(ctx, log_n);
+    launch_pow_table(ctx->pow_lo, ctx->pow_hi, log_n, offset, 1u, ctx->stream);
+    p.pre_lo = ctx->pow_lo;
+    p.pre_hi = ctx->pow_hi;
+    launch_ntt(p, ctx->scratch_a, d, ctx->scratch_b, ctx->stream);
+    FRI_HIP(ctx, hipGetLastError());
+    FRI_HIP(ctx, hipMemcpyAsync(evals_out, ctx->scratch_b, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return FRI_OK;
+}
+
+extern "C" int fri_interpolate(fri_ctx* ctx, const uint32_t* ys, uint32_t log_n, uint32_t offset,
+                               uint32_t* coeffs_out, size_t* len_out) {
+    if (!ctx || !ys || !coeffs_out || !len_out) return fail(ctx, FRI_EINVAL, "null argument");
+    if (log_n > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n exceeds context capacity");
+    if (offset == 0 || offset >= P) return fail(ctx, FRI_EINVAL, "offset must be a nonzero canonical element");
+    const size_t n = (size_t)1 << log_n;
+    if (!check_canonical(ys, n)) return fail(ctx, FRI_EINVAL, "value not canonical (>= p)");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, ys, n * 4, hipMemcpyHostToDevice, ctx->stream));
+    NttPlan p{};
+    p.log_n = log_n;
+    p.tw = ctx->tw_inv;
+    p.log_tw = ctx->log_n_max;
+    // coeff_j = n^-1 * offset^-j * sum_i ys_i w^-ij
+    launch_pow_table(ctx->pow_lo, ctx->pow_hi, log_n, inv_std(offset), inv_std((uint32_t)(n % P)), ctx->stream);
+    p.post_lo = ctx->pow_lo;
+    p.post_hi = ctx->pow_hi;
+    launch_ntt(p, ctx->scratch_a, n, ctx->scratch_b, ctx->stream);
+    FRI_HIP(ctx, hipGetLastError());
+    FRI_HIP(ctx, hipMemcpyAsync(coeffs_out, ctx->scratch_b, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    size_t len = n;
+    while (len > 0 && coeffs_out[len - 1] == 0) len--;          // Polynomial::new trim (ops.rs:19-37)
+    *len_out = len;
+    return FRI_OK;
+}
+
+extern "C" int fri_evaluate(fri_ctx* ctx, const uint32_t* coeffs, size_t d, const uint32_t* xs, size_t count,
+                            uint32_t* out) {
+    if (!ctx || (d && !coeffs) || (count && (!xs || !out))) return fail(ctx, FRI_EINVAL, "null argument");
+    const size_t cap = (size_t)1 << ctx->log_n_max;
+    if (d > cap || count > cap) return fail(ctx, FRI_EINVAL, "size exceeds context capacity");
+    if (!check_canonical(coeffs, d) || !check_canonical(xs, count))
+        return fail(ctx, FRI_EINVAL, "value not canonical (>= p)");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    if (d) FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, coeffs, d * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (count) FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_b, xs, count * 4, hipMemcpyHostToDevice, ctx->stream));
+    launch_evaluate(ctx->scratch_a, d, ctx->scratch_b, count, ctx->scratch_c, ctx->stream);
+    FRI_HIP(ctx, hipGetLastError());
+    if (count) FRI_HIP(ctx, hipMemcpyAsync(out, ctx->scratch_c, count * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return FRI_OK;
+}
+
+extern "C" int fri_fold(fri_ctx* ctx, const uint32_t* layer, uint32_t log_m, uint32_t layer_offset, uint32_t beta,
+                        uint32_t* out) {
+    if (!ctx || !layer || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    if (log_m < 1 || log_m > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_m out of range");
+    if (layer_offset == 0 || layer_offset >= P || beta >= P) return fail(ctx, FRI_EINVAL, "bad offset/beta");
+    const size_t m = (size_t)1 << log_m;
+    if (!check_canonical(layer, m)) return fail(ctx, FRI_EINVAL, "value not canonical (>= p)");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, layer, m * 4, hipMemcpyHostToDevice, ctx->stream));
+    launch_coset_points(ctx->scratch_b, m / 2, layer_offset, log_m, ctx->stream);
+    launch_batch_inverse(ctx->scratch_b, ctx->scratch_c, m / 2, 1, ctx->stream);
+    launch_fold_plain(ctx->scratch_a, ctx->scratch_b, log_m, ctx->scratch_c, beta, ctx->stream);
+    FRI_HIP(ctx, hipGetLastError());
+    FRI_HIP(ctx, hipMemcpyAsync(out, ctx->scratch_b, (m / 2) * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return FRI_OK;
+}
+
+static void digest_to_bytes(const uint32_t* w, uint8_t* out) {
+    for (int i = 0; i < 8; i++) {
+        out[4 * i] = (uint8_t)(w[i] >> 24); out[4 * i + 1] = (uint8_t)(w[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(w[i] >> 8); out[4 * i + 3] = (uint8_t)w[i];
+    }
+}
+
+// Non-power-of-two trees (rs_merkle promotes a lone right-most node).
+__global__ void k_leaf_generic(const uint32_t* v, uint32_t* out, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) sha::leaf(v[i], out + 8 * i);
+}
+__global__ void k_level_generic(const uint32_t* in, uint32_t* out, size_t cnt) {
+    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t pc = (cnt + 1) / 2;
+    if (j >= pc) return;
+    if (2 * j + 1 < cnt) sha::node(in + 16 * j, in + 16 * j + 8, out + 8 * j);
+    else for (int i = 0; i < 8; i++) out[8 * j + i] = in[16 * j + i];
+}
+
+extern "C" int fri_merkle_root(fri_ctx* ctx, const uint32_t* values, size_t n, uint8_t root32[32]) {
+    if (!ctx || !values || !root32) return fail(ctx, FRI_EINVAL, "null argument");
+    if (n == 0) return fail(ctx, FRI_EINVAL, "empty tree has no root (merkle/mod.rs:25)");
+    const size_t cap = (size_t)1 << ctx->log_n_max;
+    if (n > cap) return fail(ctx, FRI_EINVAL, "size exceeds context capacity");
+    if (!check_canonical(values, n)) return fail(ctx, FRI_EINVAL, "value not canonical (>= p)");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, values, n * 4, hipMemcpyHostToDevice, ctx->stream));
+    uint32_t* root_dev;
+    uint32_t* tree = nullptr;
+    bool pow2 = (n & (n - 1)) == 0;
+    if (pow2) {
+        uint32_t L = 0;
+        while (((size_t)1 << L) < n) L++;
+        FRI_HIP(ctx, hipMalloc(&tree, (((size_t)2 << L)) * 32));
+        launch_merkle_tree(ctx->scratch_a, tree, L, nullptr, -1, ctx->stream);
+        root_dev = tree + 8 * level_offset(L, L);
+    } else {
+        size_t total = 0;
+        for (size_t m = n;; m = (m + 1) / 2) { total += m; if (m == 1) break; }
+        FRI_HIP(ctx, hipMalloc(&tree, total * 32));
+        uint32_t* cur = tree;
+        hipLaunchKernelGGL(k_leaf_generic, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                           ctx->scratch_a, cur, n);
+        size_t cnt = n;
+        while (cnt > 1) {
+            size_t pc = (cnt + 1) / 2;
+            uint32_t* nxt = cur + 8 * cnt;
+            hipLaunchKernelGGL(k_level_generic, dim3((unsigned)((pc + 255) / 256)), dim3(256), 0, ctx->stream, cur,
+                               nxt, cnt);
+            cur = nxt;
+            cnt = pc;
+        }
+        root_dev = cur;
+    }
+    FRI_HIP(ctx, hipGetLastError());
+    uint32_t w[8];
+    hipError_t e1 = hipMemcpyAsync(w, root_dev, 32, hipMemcpyDeviceToHost, ctx->stream);
+    hipError_t e2 = hipStreamSynchronize(ctx->stream);
+    hipFree(tree);
+    FRI_HIP(ctx, e1);
+    FRI_HIP(ctx, e2);
+    digest_to_bytes(w, root32);
+    return FRI_OK;
+}
+
+// ------------------------------------------------------------- commit ----
+static int rounds_bound(size_t d, uint32_t log_n) {
+    if (d <= 1) return 0;
+    int b = 0;
+    for (size_t v = d - 1; v; v >>= 1) b++;
+    return b < (int)log_n ? b : (int)log_n;
+}
+
+static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset) {
+    Plan& p = ctx->plan;
+    if (p.valid && p.d == d && p.log_n == log_n && p.offset == offset) return FRI_OK;
+    plan_free(ctx);
+    const size_t n = (size_t)1 << log_n;
+    p.log_n = log_n;
+    p.d = d;
+    p.offset = offset;
+    p.rmax = rounds_bound(d, log_n);
+    size_t lay = 0, tre = 0, xin = 0;
+    for (int k = 0; k <= p.rmax; k++) {
+        uint32_t L = log_n - (uint32_t)k;
+        p.layer_off[k] = lay;
+        p.tree_off[k] = tre;
+        p.xinv_off[k] = xin;
+        lay += (size_t)1 << L;
+        tre += 8 * (((size_t)2 << L) - 1);
+        if (k < p.rmax) xin += ((size_t)1 << L) / 2;
+    }
+    p.layer_off[p.rmax + 1] = lay;
+    p.tree_off[p.rmax + 1] = tre;
+    p.in_cap = d ? d : 1;
+    p.coef_cap = d / 2 + 1;
+    const size_t nhi = log_n > POW_LO_LOG ? ((size_t)1 << (log_n - POW_LO_LOG)) : 1;
+    if (hipMalloc(&p.d_in, p.in_cap * 4) != hipSuccess || hipMalloc(&p.coefA, p.coef_cap * 4) != hipSuccess ||
+        hipMalloc(&p.coefB, p.coef_cap * 4) != hipSuccess || hipMalloc(&p.layers, lay * 4) != hipSuccess ||
+        hipMalloc(&p.trees, tre * 4) != hipSuccess || hipMalloc(&p.xinv, (xin ? xin : 1) * 4) != hipSuccess ||
+        hipMalloc(&p.pre_lo, ((size_t)1 << POW_LO_LOG) * 4) != hipSuccess ||
+        hipMalloc(&p.pre_hi, nhi * 4) != hipSuccess) {
+        plan_free(ctx);
+        return fail(ctx, FRI_ENOMEM, "device allocation failed for commit plan");
+    }
+    hipStream_t s = ctx->stream;
+    launch_pow_table(p.pre_lo, p.pre_hi, log_n, offset, 1u, s);
+    if (p.rmax > 0) {
+        // Domain inverses for every fold, built with the batch-inverse kernel:
+        // xinv_0[i] = (offset*w_n^i)^-1, xinv_k[i] = xinv_{k-1}[i]^2 (D_k = D_{k-1}^2).
+        launch_coset_points(ctx->scratch_a, n / 2, offset, log_n, s);
+        launch_batch_inverse(ctx->scratch_a, p.xinv + p.xinv_off[0], n / 2, 1, s);
+        for (int k = 1; k < p.rmax; k++)
+            launch_square_mont(p.xinv + p.xinv_off[k - 1], p.xinv + p.xinv_off[k], ((size_t)1 << (log_n - k)) / 2, s);
+    }
+    FRI_HIP(ctx, hipGetLastError());
+    FRI_HIP(ctx, hipStreamSynchronize(s));
+    p.valid = true;
+    return FRI_OK;
+}
+
+static const uint32_t* root_ptr(const Plan& p, int k) {
+    uint32_t L = p.log_n - (uint32_t)k;
+    return p.trees + p.tree_off[k] + 8 * level_offset(L, L);
+}
+
+// Enqueue the whole commit on ctx->stream (captured into a graph or eager).
+static void enqueue_commit(fri_ctx* ctx) {
+    Plan& p = ctx->plan;
+    hipStream_t s = ctx->stream;
+    const uint32_t log_n = p.log_n;
+    const size_t n = (size_t)1 << log_n;
+    size_t sp;
+    sp = span_begin(ctx, "degree", p.d * 4);
+    launch_degree0(p.d_in, p.d, ctx->d_state, s);
+    span_end(ctx, sp);
+    NttPlan np = lde_plan(ctx, log_n);
+    np.pre_lo = p.pre_lo;
+    np.pre_hi = p.pre_hi;
+    sp = span_begin(ctx, "lde", p.d * 4 + n * 4);
+    launch_ntt(np, p.d_in, p.d, p.layers + p.layer_off[0], s);
+    span_end(ctx, sp);
+    // Algorithmic bytes of a merkle_leaf launch over 2^L values: read 4 B per
+    // value, write every digest of the levels it builds (32 B each).
+    auto tree_bytes = [](uint32_t L) -> uint64_t {
+        uint32_t h = L < SUBTREE_LOG ? L : SUBTREE_LOG;
+        uint64_t nodes = 0;
+        for (uint32_t j = 0; j <= h; j++) nodes += (uint64_t)1 << (L - j);
+        return ((uint64_t)4 << L) + 32 * nodes;
+    };
+    // Layer-0 tree: the leaf kernel (dominant kernel of the commit) is timed
+    // on its own; its span ends right after the leaf launch.
+    size_t spl = span_begin(ctx, "merkle_layer0_leaf", tree_bytes(log_n));
+    launch_merkle_tree(p.layers + p.layer_off[0], p.trees + p.tree_off[0], log_n, ctx->d_state, -1, s, nullptr,
+                       spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
+    sp = span_begin(ctx, "channel", 0);
+    launch_channel_step(ctx->d_state, 0, p.d_in, root_ptr(p, 0), log_n, s);
+    span_end(ctx, sp);
+    for (int r = 0; r < p.rmax; r++) {
+        uint32_t L = log_n - (uint32_t)r;
+        sp = span_begin(ctx, "fold", ((uint64_t)4 << L) + ((uint64_t)2 << L) + ((uint64_t)2 << L));
+        launch_fold_round(p.layers + p.layer_off[r], p.layers + p.layer_off[r + 1], L, p.xinv + p.xinv_off[r],
+                          ctx->d_state, r, s);
+        span_end(ctx, sp);
+        const uint32_t* csrc = (r == 0) ? p.d_in : ((r - 1) % 2 == 0 ? p.coefA : p.coefB);
+        uint32_t* cdst = (r % 2 == 0) ? p.coefA : p.coefB;
+        size_t cap = (p.d + ((size_t)2 << r) - 1) >> (r + 1);
+        sp = span_begin(ctx, "coeff_fold", cap * 12);
+        launch_coeff_fold(csrc, cdst, cap, ctx->d_state, r, s);
+        span_end(ctx, sp);
+        sp = span_begin(ctx, "merkle", tree_bytes(L - 1));
+        launch_merkle_tree(p.layers + p.layer_off[r + 1], p.trees + p.tree_off[r + 1], L - 1, ctx->d_state, r, s);
+        span_end(ctx, sp);
+        sp = span_begin(ctx, "channel", 0);
+        launch_channel_step(ctx->d_state, r + 1, cdst, root_ptr(p, r + 1), L - 1, s);
+        span_end(ctx, sp);
+    }
+}
+
+static void init_state(fri_ctx* ctx, const fri_channel_state* chan_in, uint32_t flags,
+                       const uint32_t* forced_betas) {
+    DevState* h = ctx->h_state;
+    memset(h, 0, sizeof(DevState));
+    if (chan_in && chan_in->has_state) {
+        for (int i = 0; i < 8; i++)
+            h->chan[i] = ((uint32_t)chan_in->digest[4 * i] << 24) | ((uint32_t)chan_in->digest[4 * i + 1] << 16) |
+                         ((uint32_t)chan_in->digest[4 * i + 2] << 8) | chan_in->digest[4 * i + 3];
+        h->chan_has = 1;
+    }
+    h->deg0max = -1;
+    h->final_degree = -1;
+    for (int r = 0; r < MAXR; r++) { h->newmax[r] = -1; h->evenmax[r] = -1; h->oddmax[r] = -1; }
+    for (int r = 0; r <= MAXR; r++) h->deg[r] = -1;
+    if ((flags & FRI_FLAG_FORCE_BETAS) && forced_betas) {
+        h->forced = 1;
+        for (int r = 0; r < MAXR; r++) h->forced_beta[r] = forced_betas[r];
+    }
+}
+
+static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
+                      uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                      const uint32_t* forced_betas, fri_commit_result* out) {
+    if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    if (log_n < 1 || log_n > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n out of range for context");
+    const size_t n = (size_t)1 << log_n;
+    if (d > n) return fail(ctx, FRI_EDEGREE, "more coefficients than domain points (domain would be exhausted)");
+    if (offset == 0 || offset >= P) return fail(ctx, FRI_EINVAL, "offset must be a nonzero canonical element");
+    if ((flags & FRI_FLAG_FORCE_BETAS) && !forced_betas) return fail(ctx, FRI_EINVAL, "forced betas missing");
+    if (host_coeffs && !check_canonical(host_coeffs, d)) return fail(ctx, FRI_EINVAL, "coefficient not canonical");
+    if (forced_betas && (flags & FRI_FLAG_FORCE_BETAS) && !check_canonical(forced_betas, MAXR))
+        return fail(ctx, FRI_EINVAL, "forced beta not canonical");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = plan_build(ctx, d, log_n, offset);
+    if (rc) return rc;
+    Plan& p = ctx->plan;
+    hipStream_t s = ctx->stream;
+    init_state(ctx, chan_in, flags, forced_betas);
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
+    if (host_coeffs && d)
+        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
+    else if (dev_coeffs && dev_coeffs != p.d_in && d)
+        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, s));
+    const bool use_graph = !(flags & FRI_FLAG_NO_GRAPH) && !ctx->profiling;
+    if (use_graph) {
+        if (!p.exec) {
+            FRI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            enqueue_commit(ctx);
+            hipGraph_t g = nullptr;
+            FRI_HIP(ctx, hipStreamEndCapture(s, &g));
+            p.graph = g;
+            FRI_HIP(ctx, hipGraphInstantiate(&p.exec, g, nullptr, nullptr, 0));
+        }
+        FRI_HIP(ctx, hipGraphLaunch(p.exec, s));
+    } else {
+        enqueue_commit(ctx);
+        FRI_HIP(ctx, hipGetLastError());
+    }
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
+    FRI_HIP(ctx, hipStreamSynchronize(s));
+    if (ctx->profiling) spans_collect(ctx);
+    const DevState* h = ctx->h_state;
+    if (h->status) return fail(ctx, (int)h->status, "degree exceeds the domain (reference would panic)");
+    memset(out, 0, sizeof *out);
+    out->n_layers = h->n_layers;
+    out->n_rounds = h->n_rounds;
+    out->log_n = log_n;
+    out->final_value = h->final_value;
+    out->final_degree = h->final_degree;
+    for (uint32_t k = 0; k < h->n_layers && k <= (uint32_t)MAXR; k++) digest_to_bytes(h->roots[k], out->roots[k]);
+    for (uint32_t r = 0; r < h->n_rounds && r < (uint32_t)MAXR; r++) out->betas[r] = h->beta[r];
+    digest_to_bytes(h->chan, out->channel_out.digest);
+    out->channel_out.has_state = h->chan_has;
+    ctx->err.clear();
+    return FRI_OK;
+}
+
+extern "C" int fri_commit(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n, uint32_t offset,
+                          const fri_channel_state* chan_in, uint32_t flags, const uint32_t* forced_betas,
+                          fri_commit_result* out) {
+    if (d && !coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    return run_commit(ctx, coeffs, nullptr, d, log_n, offset, chan_in, flags, forced_betas, out);
+}
+
+extern "C" int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
+                                 uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                                 const uint32_t* forced_betas, fri_commit_result* out) {
+    if (d && !d_coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    return run_commit(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
+}
+
+extern "C" int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr) {
+    if (!ctx || !d_ptr) return fail(ctx, FRI_EINVAL, "null argument");
+    // The plan's input buffer is only stable for a fixed (d, log_n, offset);
+    // the caller passes the returned pointer back to fri_commit_device, which
+    // skips the copy when the pointers match.
+    if (!ctx->plan.valid || ctx->plan.d != d) return fail(ctx, FRI_ESTATE, "build a plan first (commit once with this d)");
+    *d_ptr = ctx->plan.d_in;
+    return FRI_OK;
+}
+
+extern "C" int fri_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out, size_t cap) {
+    if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    const Plan& p = ctx->plan;
+    if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
+    size_t m = (size_t)1 << (p.log_n - layer);
+    if (cap < m) return fail(ctx, FRI_EINVAL, "output buffer too small");
+    FRI_HIP(ctx, hipMemcpy(out, p.layers + p.layer_off[layer], m * 4, hipMemcpyDeviceToHost));
+    return FRI_OK;
+}
+
+extern "C" int fri_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level, uint8_t* out, size_t cap) {
+    if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    const Plan& p = ctx->plan;
+    if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
+    uint32_t L = p.log_n - layer;
+    if (level > L) return fail(ctx, FRI_EINVAL, "level above root");
+    size_t cnt = (size_t)1 << (L - level);
+    if (cap < cnt * 32) return fail(ctx, FRI_EINVAL, "output buffer too small");
+    std::vector<uint32_t> w(cnt * 8);
+    FRI_HIP(ctx, hipMemcpy(w.data(), p.trees + p.tree_off[layer] + 8 * level_offset(L, level), cnt * 32,
+                           hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < cnt; i++) digest_to_bytes(&w[8 * i], out + 32 * i);
+    return FRI_OK;
+}
+
+extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint32_t* value_out, uint8_t* path,
+                             uint32_t* depth_out) {
+    if (!ctx || !value_out || !depth_out) return fail(ctx, FRI_EINVAL, "null argument");
+    const Plan& p = ctx->plan;
+    if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
+    uint32_t L = p.log_n - layer;
+    if (index >> L) return fail(ctx, FRI_EINVAL, "index out of range");
+    FRI_HIP(ctx, hipMemcpy(value_out, p.layers + p.layer_off[layer] + index, 4, hipMemcpyDeviceToHost));
+    for (uint32_t l = 0; l < L && path; l++) {
+        uint64_t sib = (index >> l) ^ 1u;
+        uint32_t w[8];
+        FRI_HIP(ctx, hipMemcpy(w, p.trees + p.tree_off[layer] + 8 * (level_offset(L, l) + sib), 32,
+                               hipMemcpyDeviceToHost));
+        digest_to_bytes(w, path + 32 * l);
+    }
+    *depth_out = L;
+    return FRI_OK;
+}
+
+extern "C" int fri_set_profiling(fri_ctx* ctx, int enabled) {
+    if (!ctx) return FRI_EINVAL;
+    ctx->profiling = enabled != 0;
+    return FRI_OK;
+}
+extern "C" int fri_get_profile(fri_ctx* ctx, const char* cls, double* total_ms, uint64_t* launches,
+                               uint64_t* bytes) {
+    if (!ctx || !cls) return FRI_EINVAL;
+    auto it = ctx->prof.find(cls);
+    if (it == ctx->prof.end()) {
+        if (total_ms) *total_ms = 0;
+        if (launches) *launches = 0;
+        if (bytes) *bytes = 0;
+        return FRI_OK;
+    }
+    if (total_ms) *total_ms = it->second.ms;
+    if (launches) *launches = it->second.launches;
+    if (bytes) *bytes = it->second.bytes;
+    return FRI_OK;
+}
+extern "C" int fri_reset_profile(fri_ctx* ctx) {
+    if (!ctx) return FRI_EINVAL;
+    ctx->prof.clear();
+    return FRI_OK;
+}

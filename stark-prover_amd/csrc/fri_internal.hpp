@@ -1,0 +1,89 @@
+// fri_internal.hpp — device state layout and kernel launchers shared by
+// fri_kernels.hip (kernels) and fri_api.hip (context / C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include "field.hpp"
+
+namespace fri {
+
+constexpr int MAXR = 32;            // == FRI_MAX_ROUNDS
+constexpr uint32_t NTT_TILE_LOG = 12;   // first-pass LDS tile: 4096 elements
+constexpr uint32_t NTT_MID_LOG = 10;    // middle-pass stages per launch
+constexpr uint32_t NTT_MID_W = 16;      // middle-pass contiguous run (64 B)
+constexpr uint32_t SUBTREE_LOG = 9;     // Merkle subtree per workgroup: 512 items (1 node per lane per level)
+constexpr uint32_t POW_LO_LOG = 12;     // two-level power tables s^j = lo[j&4095]*hi[j>>12]
+
+// Device-resident commit state (one per context).  Every per-round kernel
+// reads its gate (active[r]) and operands (beta, degrees) from here, so the
+// whole commit is a static launch sequence that a hipGraph can replay and
+// that needs no host round trip between Fiat-Shamir rounds.
+struct DevState {
+    uint32_t chan[8];            // channel state digest (src/channel/channel.rs:19)
+    uint32_t chan_has;           // 0 => state == ""
+    uint32_t n_layers;
+    uint32_t n_rounds;
+    uint32_t final_value;
+    int32_t  final_degree;
+    uint32_t status;             // 0 ok, else FRI_E* raised on device
+    uint32_t forced;             // FRI_FLAG_FORCE_BETAS
+    int32_t  deg0max;            // max nonzero index of the input coefficients
+    uint32_t active[MAXR + 1];   // active[r]: fold round r runs (deg_r >= 1)
+    int32_t  deg[MAXR + 1];      // degree of poly_k (reference degree field)
+    int32_t  newmax[MAXR];       // per round: max j with folded c'_j != 0
+    int32_t  evenmax[MAXR];      //            max j with c_{2j}   != 0
+    int32_t  oddmax[MAXR];       //            max j with c_{2j+1} != 0
+    uint32_t beta[MAXR];
+    uint32_t beta_mont[MAXR];
+    uint32_t forced_beta[MAXR];
+    uint32_t roots[MAXR + 1][8];
+};
+
+// Tree layout: layer with 2^L leaves stores levels 0..L contiguously,
+// level l at digest offset 2^(L+1) - 2^(L+1-l) (8 words per digest).
+__host__ __device__ inline size_t level_offset(uint32_t L, uint32_t l) {
+    return ((size_t)2 << L) - ((size_t)2 << (L - l));
+}
+
+// ---- launchers (fri_kernels.hip); all asynchronous on `s` ----------------
+struct NttPlan {
+    uint32_t log_n;              // transform size 2^log_n
+    const uint32_t* tw;          // Montgomery twiddles w_{2^log_tw}^j, j < 2^(log_tw-1)
+    uint32_t log_tw;
+    const uint32_t* pre_lo;      // optional input scale s^j (Montgomery, two-level)
+    const uint32_t* pre_hi;
+    const uint32_t* post_lo;     // optional output scale t^j (Montgomery, two-level)
+    const uint32_t* post_hi;
+};
+// dst[k] = post(k) * sum_{j<d} src[j]*pre(j)*w^(jk); src may alias nothing in dst.
+void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, hipStream_t s);
+
+void launch_twiddles(uint32_t* tw, uint32_t log_tw, bool inverse, hipStream_t s);
+void launch_pow_table(uint32_t* lo, uint32_t* hi, uint32_t log_n, uint32_t base_std,
+                      uint32_t scale_std, hipStream_t s);
+void launch_batch_inverse(const uint32_t* in, uint32_t* out, size_t n, int out_mont,
+                          hipStream_t s);
+void launch_coset_points(uint32_t* out, size_t count, uint32_t offset, uint32_t log_n,
+                         hipStream_t s);
+void launch_square_mont(const uint32_t* in, uint32_t* out, size_t count, hipStream_t s);
+void launch_evaluate(const uint32_t* coeffs, size_t d, const uint32_t* xs, size_t count,
+                     uint32_t* out, hipStream_t s);
+void launch_fold_plain(const uint32_t* in, uint32_t* out, uint32_t log_m, const uint32_t* xinv_m,
+                       uint32_t beta, hipStream_t s);
+
+// Merkle: hash layer (2^L values) into its tree (all levels).
+void launch_merkle_tree(const uint32_t* values, uint32_t* tree, uint32_t L,
+                        const DevState* st, int gate_round, hipStream_t s,
+                        hipEvent_t ev_leaf_begin = nullptr, hipEvent_t ev_leaf_end = nullptr);
+
+// Commit-path kernels gated on st->active[r].
+void launch_degree0(const uint32_t* coeffs, size_t d, DevState* st, hipStream_t s);
+void launch_fold_round(const uint32_t* in, uint32_t* out, uint32_t log_m, const uint32_t* xinv_m,
+                       const DevState* st, int r, hipStream_t s);
+void launch_coeff_fold(const uint32_t* c, uint32_t* cn, size_t cap, DevState* st, int r,
+                       hipStream_t s);
+void launch_channel_step(DevState* st, int k, const uint32_t* coef_k, const uint32_t* root,
+                         uint32_t log_n_k, hipStream_t s);
+
+}  // namespace fri

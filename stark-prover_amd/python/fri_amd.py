@@ -1,0 +1,354 @@
+"""fri_amd — Python host mirror of the reference FRI-commit interface over
+``libfri_amd.so`` (C ABI: include/fri_amd.h).
+
+Mirrors the reference crate's surface for this path (same names, argument
+meaning, error behaviour):
+
+* ``Channel``            — src/channel/channel.rs (send / receive_random_field_element /
+                           receive_random_int / proof / proof_size)
+* ``MerkleTree``         — src/merkle/mod.rs (``MerkleTree(values).root() -> hex str``)
+* ``fri_commit``         — src/fri/fri_commit.rs:72-122, returns ``FRIProof``
+* ``lde`` / ``interpolate`` / ``evaluate`` / ``batch_inverse`` / ``fold`` — the
+  polynomial / field kernels (src/polynomial/ops.rs, interpolation.rs,
+  src/fields/element.rs, src/fri/fri_commit.rs:53-65).
+
+Every compute call goes through the HIP library; there is no CPU fallback.
+If the library or a gfx950 GPU is missing the calls raise ``FriError``.
+Where the reference panics, these raise ``FriError`` as well.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+P = 3221225473
+GENERATOR = 5
+MAX_ROUNDS = 32
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libfri_amd.so"))
+HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "fri_amd.h"))
+
+FRI_OK, FRI_EINVAL, FRI_ENOMEM, FRI_EHIP, FRI_ENODEV, FRI_ERCCL, FRI_ESTATE, FRI_EDEGREE = range(8)
+FLAG_FORCE_BETAS = 1
+FLAG_NO_GRAPH = 2
+
+
+class FriError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"fri_amd error {code}: {msg}")
+        self.code = code
+
+
+class ChannelState(ctypes.Structure):
+    _fields_ = [("digest", ctypes.c_uint8 * 32), ("has_state", ctypes.c_uint32)]
+
+
+class CommitResult(ctypes.Structure):
+    _fields_ = [("n_layers", ctypes.c_uint32), ("n_rounds", ctypes.c_uint32), ("log_n", ctypes.c_uint32),
+                ("final_value", ctypes.c_uint32), ("final_degree", ctypes.c_int32),
+                ("reserved", ctypes.c_uint32),
+                ("roots", (ctypes.c_uint8 * 32) * (MAX_ROUNDS + 1)),
+                ("betas", ctypes.c_uint32 * MAX_ROUNDS),
+                ("channel_out", ChannelState)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libfri_amd.so; raises FriError if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FriError(FRI_ENODEV, f"{path} missing: build it with `make -C stark-prover_amd`")
+    lib = ctypes.CDLL(path)
+    u32, sz, i32 = ctypes.c_uint32, ctypes.c_size_t, ctypes.c_int
+    pu32 = ctypes.POINTER(ctypes.c_uint32)
+    vp = ctypes.c_void_p
+    sig = {
+        "fri_ctx_create": (i32, [i32, u32, ctypes.POINTER(vp)]),
+        "fri_ctx_destroy": (i32, [vp]),
+        "fri_last_error": (ctypes.c_char_p, [vp]),
+        "fri_version": (ctypes.c_char_p, []),
+        "fri_batch_inverse": (i32, [vp, pu32, pu32, sz]),
+        "fri_lde": (i32, [vp, pu32, sz, u32, u32, pu32]),
+        "fri_interpolate": (i32, [vp, pu32, u32, u32, pu32, ctypes.POINTER(sz)]),
+        "fri_evaluate": (i32, [vp, pu32, sz, pu32, sz, pu32]),
+        "fri_fold": (i32, [vp, pu32, u32, u32, u32, pu32]),
+        "fri_merkle_root": (i32, [vp, pu32, sz, ctypes.c_char_p]),
+        "fri_commit": (i32, [vp, pu32, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
+                             ctypes.POINTER(CommitResult)]),
+        "fri_commit_device": (i32, [vp, vp, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
+                                    ctypes.POINTER(CommitResult)]),
+        "fri_ctx_input_buffer": (i32, [vp, sz, ctypes.POINTER(vp)]),
+        "fri_layer_copy": (i32, [vp, u32, pu32, sz]),
+        "fri_tree_level_copy": (i32, [vp, u32, u32, ctypes.c_char_p, sz]),
+        "fri_auth_path": (i32, [vp, u32, ctypes.c_uint64, pu32, ctypes.c_char_p, ctypes.POINTER(u32)]),
+        "fri_set_profiling": (i32, [vp, i32]),
+        "fri_get_profile": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+        "fri_reset_profile": (i32, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _u32(a) -> np.ndarray:
+    arr = np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+    if arr.size and int(arr.max()) >= P:
+        raise FriError(FRI_EINVAL, "field element not canonical (>= p)")
+    return np.ascontiguousarray(arr.astype(np.uint32))
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
+class Context:
+    """Owns one fri_ctx (device buffers, stream, graphs) on one GPU."""
+
+    def __init__(self, device: int = 0, log_n_max: int = 20):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.fri_ctx_create(device, log_n_max, ctypes.byref(h))
+        if rc != FRI_OK:
+            raise FriError(rc, "fri_ctx_create failed (no gfx950 device?)")
+        self.h = h
+        self.log_n_max = log_n_max
+
+    def close(self):
+        if self.h:
+            self.lib.fri_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != FRI_OK:
+            raise FriError(rc, self.lib.fri_last_error(self.h).decode())
+
+    # ---- kernel-level ops ------------------------------------------------
+    def batch_inverse(self, xs) -> np.ndarray:
+        a = _u32(xs)
+        out = np.empty_like(a)
+        self._check(self.lib.fri_batch_inverse(self.h, _ptr(a), _ptr(out), a.size))
+        return out
+
+    def lde(self, coeffs, log_n: int, offset: int = GENERATOR) -> np.ndarray:
+        c = _u32(coeffs)
+        out = np.empty(1 << log_n, dtype=np.uint32)
+        self._check(self.lib.fri_lde(self.h, _ptr(c), c.size, log_n, offset, _ptr(out)))
+        return out
+
+    def interpolate(self, ys, offset: int = GENERATOR) -> np.ndarray:
+        y = _u32(ys)
+        log_n = int(y.size).bit_length() - 1
+        if y.size != 1 << log_n:
+            raise FriError(FRI_EINVAL, "coset interpolation needs a power-of-two point count")
+        out = np.empty(y.size, dtype=np.uint32)
+        ln = ctypes.c_size_t()
+        self._check(self.lib.fri_interpolate(self.h, _ptr(y), log_n, offset, _ptr(out), ctypes.byref(ln)))
+        return out[: ln.value]
+
+    def evaluate(self, coeffs, xs) -> np.ndarray:
+        c, x = _u32(coeffs), _u32(xs)
+        out = np.empty(x.size, dtype=np.uint32)
+        self._check(self.lib.fri_evaluate(self.h, _ptr(c), c.size, _ptr(x), x.size, _ptr(out)))
+        return out
+
+    def fold(self, layer, layer_offset: int, beta: int) -> np.ndarray:
+        v = _u32(layer)
+        log_m = int(v.size).bit_length() - 1
+        out = np.empty(v.size // 2, dtype=np.uint32)
+        self._check(self.lib.fri_fold(self.h, _ptr(v), log_m, layer_offset, beta, _ptr(out)))
+        return out
+
+    def merkle_root(self, values) -> bytes:
+        v = _u32(values)
+        root = ctypes.create_string_buffer(32)
+        self._check(self.lib.fri_merkle_root(self.h, _ptr(v), v.size, root))
+        return root.raw
+
+    # ---- commit ----------------------------------------------------------
+    def commit(self, coeffs, log_n: int, offset: int = GENERATOR, channel_state: Optional[bytes] = None,
+               forced_betas: Optional[Sequence[int]] = None, graph: bool = True) -> CommitResult:
+        c = _u32(coeffs)
+        ch = ChannelState()
+        if channel_state:
+            ctypes.memmove(ch.digest, channel_state, 32)
+            ch.has_state = 1
+        flags = 0 if graph else FLAG_NO_GRAPH
+        fb = None
+        if forced_betas is not None:
+            fbarr = np.zeros(MAX_ROUNDS, dtype=np.uint32)
+            fbarr[: len(forced_betas)] = forced_betas
+            fb = fbarr
+            flags |= FLAG_FORCE_BETAS
+        res = CommitResult()
+        self._check(self.lib.fri_commit(self.h, _ptr(c), c.size, log_n, offset, ctypes.byref(ch), flags,
+                                        _ptr(fb) if fb is not None else None, ctypes.byref(res)))
+        return res
+
+    def layer(self, k: int, log_n: int) -> np.ndarray:
+        out = np.empty(1 << (log_n - k), dtype=np.uint32)
+        self._check(self.lib.fri_layer_copy(self.h, k, _ptr(out), out.size))
+        return out
+
+    def tree_level(self, k: int, level: int, log_n: int) -> List[bytes]:
+        cnt = 1 << (log_n - k - level)
+        buf = ctypes.create_string_buffer(32 * cnt)
+        self._check(self.lib.fri_tree_level_copy(self.h, k, level, buf, 32 * cnt))
+        raw = buf.raw
+        return [raw[32 * i: 32 * i + 32] for i in range(cnt)]
+
+    def auth_path(self, k: int, index: int, log_n: int):
+        depth = log_n - k
+        buf = ctypes.create_string_buffer(32 * max(depth, 1))
+        val = ctypes.c_uint32()
+        dep = ctypes.c_uint32()
+        self._check(self.lib.fri_auth_path(self.h, k, index, ctypes.byref(val), buf, ctypes.byref(dep)))
+        return val.value, [buf.raw[32 * i: 32 * i + 32] for i in range(dep.value)]
+
+    def set_profiling(self, on: bool):
+        self._check(self.lib.fri_set_profiling(self.h, 1 if on else 0))
+
+    def profile(self, cls: str):
+        ms, n, b = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.fri_get_profile(self.h, cls.encode(), ctypes.byref(ms), ctypes.byref(n),
+                                             ctypes.byref(b)))
+        return ms.value, n.value, b.value
+
+    def reset_profile(self):
+        self._check(self.lib.fri_reset_profile(self.h))
+
+
+# ----------------------------------------------------------------------------
+# Reference-shaped host objects
+# ----------------------------------------------------------------------------
+@dataclass
+class Channel:
+    """src/channel/channel.rs — host-side transcript (authoritative state).
+
+    fri_commit() hands the state to the device, which replays the exact same
+    send/receive sequence, and then appends the same proof messages here."""
+    state: str = ""
+    proof: List[bytes] = field(default_factory=list)
+    compressed_proof: List[bytes] = field(default_factory=list)
+
+    def send(self, message: bytes) -> None:                               # channel.rs:35-44
+        self.state = hashlib.sha256((self.state + bytes(message).hex()).encode()).hexdigest()
+        self.proof.append(bytes(message))
+        self.compressed_proof.append(bytes(message))
+
+    def receive_random_int(self, lo: int, hi: int, show_in_proof: bool) -> int:   # channel.rs:58-84
+        if not self.state:
+            raise FriError(FRI_ESTATE, "Channel state is not valid hex")   # channel.rs:65
+        num = (int(self.state, 16) + lo) % ((hi - lo) + 1)
+        self.state = hashlib.sha256(self.state.encode()).hexdigest()
+        num &= (1 << 64) - 1
+        if show_in_proof:
+            self.proof.append(num.to_bytes(8, "big"))
+        return num
+
+    def receive_random_field_element(self) -> int:                        # channel.rs:47-55
+        num = self.receive_random_int(0, P - 1, False)
+        self.proof.append(num.to_bytes(8, "big"))
+        return num % P
+
+    def proof_size(self) -> int:                                          # channel.rs:88-90
+        return sum(len(b) for b in self.proof)
+
+    def compressed_proof_size(self) -> int:                               # channel.rs:93-95
+        return sum(len(b) for b in self.compressed_proof)
+
+
+class MerkleTree:
+    """src/merkle/mod.rs:5-27 — SHA-256 tree over u64-BE leaves (GPU-built)."""
+
+    def __init__(self, values: Sequence[int], ctx: Optional[Context] = None):
+        self._ctx = ctx or _default_ctx(max(1, (len(values) - 1).bit_length()))
+        self._root = self._ctx.merkle_root(values)
+
+    def root(self) -> str:
+        return self._root.hex()
+
+
+@dataclass
+class FRIProof:
+    """src/fri/fri_commit.rs:9-13 — layers/merkles read back lazily from the device."""
+    ctx: Context
+    log_n: int
+    roots: List[bytes]
+    betas: List[int]
+    final_value: int
+    final_degree: int
+
+    @property
+    def n_layers(self) -> int:
+        return len(self.roots)
+
+    def layer(self, k: int) -> np.ndarray:
+        return self.ctx.layer(k, self.log_n)
+
+    @property
+    def fri_layers(self) -> List[np.ndarray]:
+        return [self.layer(k) for k in range(self.n_layers)]
+
+    def merkle_root(self, k: int) -> str:
+        return self.roots[k].hex()
+
+    @property
+    def final_poly(self) -> List[int]:
+        return [] if self.final_degree == -1 else [self.final_value]
+
+
+_CTX_CACHE = {}
+
+
+def _default_ctx(log_n: int) -> Context:
+    key = max(log_n, 12)
+    for k, c in _CTX_CACHE.items():
+        if k >= key:
+            return c
+    c = Context(0, key)
+    _CTX_CACHE[key] = c
+    return c
+
+
+def fri_commit(coeffs: Sequence[int], log_n: int, channel: Channel, offset: int = GENERATOR,
+               ctx: Optional[Context] = None) -> FRIProof:
+    """src/fri/fri_commit.rs:72-122 on the coset domain offset*<w_{2^log_n}>.
+
+    Updates ``channel`` exactly as the reference does: proof gets
+    root_hex bytes per layer, 8-byte BE beta per round, 8-byte BE final value;
+    state ends as the device computed it."""
+    ctx = ctx or _default_ctx(log_n)
+    st = bytes.fromhex(channel.state) if channel.state else None
+    res = ctx.commit(coeffs, log_n, offset, channel_state=st)
+    roots = [bytes(res.roots[k]) for k in range(res.n_layers)]
+    betas = [int(res.betas[r]) for r in range(res.n_rounds)]
+    for k, root in enumerate(roots):
+        channel.proof.append(root.hex().encode())
+        channel.compressed_proof.append(root.hex().encode())
+        if k < len(betas):
+            channel.proof.append(betas[k].to_bytes(8, "big"))
+    fv = int(res.final_value).to_bytes(8, "big")
+    channel.proof.append(fv)
+    channel.compressed_proof.append(fv)
+    channel.state = bytes(res.channel_out.digest).hex() if res.channel_out.has_state else ""
+    return FRIProof(ctx, log_n, roots, betas, int(res.final_value), int(res.final_degree))

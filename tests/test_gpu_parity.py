@@ -1,0 +1,275 @@
+"""GPU parity: every C-ABI entry point of libfri_amd.so against the oracle
+(C restatement + Python twin) on identical inputs; bit-exact (integer field
+arithmetic + SHA-256, no tolerance).  Mirrors the reference's test style
+(src/fields/element.rs:149-290, src/polynomial/ops.rs:551-1089,
+src/polynomial/interpolation.rs:154-374) for the GPU path."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+P = 3221225473
+
+
+def rng_field(seed, n):
+    r = np.random.default_rng(seed)
+    return r.integers(0, P, size=n, dtype=np.uint64)
+
+
+def c_u64(a):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+    return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+
+# ------------------------------------------------------------------ field --
+def test_batch_inverse_matches_fermat(ctx, corc):
+    x = rng_field(1, 10007)
+    x[::97] = 0                              # inverse(0) = 0 (element.rs:54-57)
+    x[1] = 1
+    x[2] = P - 1
+    got = ctx.batch_inverse(x)
+    xs, px = c_u64(x)
+    want = np.empty_like(xs)
+    corc.orc_batch_inverse(px, want.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), xs.size, P)
+    assert np.array_equal(got.astype(np.uint64), want)
+    for i in (0, 1, 2, 3, 500, 10006):
+        assert int(got[i]) == corc.orc_fe_inverse(int(x[i]), P)
+
+
+def test_batch_inverse_edges(ctx):
+    assert ctx.batch_inverse([0]).tolist() == [0]
+    assert ctx.batch_inverse([1, 2]).tolist() == [1, (P + 1) // 2]
+    assert ctx.batch_inverse([]).tolist() == []
+
+
+# --------------------------------------------------------------- poly: LDE --
+@pytest.mark.parametrize("log_n,d", [(1, 1), (1, 2), (3, 1), (4, 2), (6, 8), (10, 128), (12, 512),
+                                     (13, 1024), (14, 2048), (16, 8192), (17, 100), (20, 1 << 17),
+                                     (22, 1 << 19), (12, 4096)])
+def test_lde_matches_oracle(ctx, corc, log_n, d):
+    c = rng_field(log_n * 100 + d, d)
+    got = ctx.lde(c, log_n, 5)
+    cs, pc = c_u64(c)
+    want = np.empty(1 << log_n, dtype=np.uint64)
+    assert corc.orc_lde(pc, d, log_n, 5, 5, P, want.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) == 0
+    assert np.array_equal(got.astype(np.uint64), want)
+
+
+def test_lde_matches_horner(ctx, corc):
+    """Config 1 analogue (benches/poly_ops.rs:161-181): Horner at every domain point."""
+    log_n, d = 10, 1 << 10
+    c = rng_field(3333, d)
+    got = ctx.lde(c, log_n, 5)
+    cs, pc = c_u64(c)
+    w = corc.orc_fe_pow(5, (P - 1) >> log_n, P)
+    for i in (0, 1, 7, 511, 512, 1023):
+        x = corc.orc_fe_mul(5, corc.orc_fe_pow(w, i, P), P)
+        assert int(got[i]) == corc.orc_poly_evaluate(pc, d, x, P)
+
+
+def test_evaluate_matches_horner(ctx, corc):
+    c = rng_field(7, 300)
+    xs = rng_field(8, 257)
+    got = ctx.evaluate(c, xs)
+    cs, pc = c_u64(c)
+    for i in range(0, 257, 16):
+        assert int(got[i]) == corc.orc_poly_evaluate(pc, 300, int(xs[i]), P)
+    assert ctx.evaluate([], [5]).tolist() == [0]          # zero poly (ops.rs:561-566)
+    assert ctx.evaluate([5], [0]).tolist() == [5]          # constant (ops.rs:568-574)
+
+
+# ------------------------------------------------------ poly: interpolate --
+@pytest.mark.parametrize("log_n", [0, 1, 2, 5, 10, 13, 16])
+def test_interpolate_roundtrip(ctx, corc, log_n):
+    n = 1 << log_n
+    c = rng_field(log_n + 5, n)
+    c[-1] = 0
+    c[-2 if n > 1 else -1] = 0
+    ys = ctx.lde(c, log_n, 5)
+    got = ctx.interpolate(ys, 5)
+    trimmed = np.trim_zeros(c.astype(np.uint64), "b")
+    assert np.array_equal(got.astype(np.uint64), trimmed)
+    ys64, py = c_u64(ys)
+    want = np.empty(n, dtype=np.uint64)
+    ln = corc.orc_interpolate_coset(py, log_n, 5, 5, P, want.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    assert np.array_equal(got.astype(np.uint64), want[:ln])
+
+
+def test_interpolate_matches_lagrange(ctx, corc, oracle):
+    """Same interpolant as the reference's Lagrange path (interpolation.rs:121-152)."""
+    log_n = 4
+    ys = rng_field(99, 1 << log_n)
+    got = ctx.interpolate(ys, 5)
+    xs = oracle.coset_domain(log_n)
+    want = oracle.interpolate_lagrange_polynomials(xs, [int(v) for v in ys], P)
+    assert got.tolist() == want
+
+
+# ---------------------------------------------------------------- fold ----
+@pytest.mark.parametrize("log_m", [1, 2, 5, 11, 16, 20])
+def test_fold_matches_coefficient_fold(ctx, corc, oracle, log_m):
+    """fri_commit.rs:53-65: coefficient fold + Horner on the squared domain."""
+    m = 1 << log_m
+    d = max(1, m // 4)
+    c = rng_field(log_m, d)
+    layer = ctx.lde(c, log_m, 5)
+    beta = int(rng_field(log_m + 1000, 1)[0])
+    got = ctx.fold(layer, 5, beta)
+    lay, pl = c_u64(layer)
+    want = np.empty(m // 2, dtype=np.uint64)
+    w = corc.orc_fe_pow(5, (P - 1) >> log_m, P)
+    corc.orc_fold_eval(pl, m, 5, w, beta, P, want.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    assert np.array_equal(got.astype(np.uint64), want)
+    if log_m <= 11:
+        poly, _ = oracle.next_fri_polynomial([int(v) for v in c], len(c) - 1, beta, P)
+        sq = corc.orc_fe_mul(5, 5, P)
+        ref = ctx.lde(poly if poly else [0], log_m - 1, sq)
+        assert np.array_equal(got, ref)
+
+
+# -------------------------------------------------------------- Merkle ----
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 13, 64, 100, 512, 513, 1024, 4096, 65536, 1 << 20])
+def test_merkle_root_matches_oracle(ctx, corc, oracle, n):
+    v = rng_field(n, n)
+    got = ctx.merkle_root(v)
+    vs, pv = c_u64(v)
+    cnt = corc.orc_merkle_nodes_count(n)
+    buf = ctypes.create_string_buffer(32 * cnt)
+    corc.orc_merkle_build(pv, n, buf)
+    assert got == buf.raw[32 * (cnt - 1):]
+    if n <= 4096:
+        assert got.hex() == oracle.merkle_root_hex([int(x) for x in v])
+
+
+def test_merkle_tree_class(oracle):
+    import fri_amd
+    vals = [1, 2, 3, 4, 5]
+    assert fri_amd.MerkleTree(vals).root() == oracle.merkle_root_hex(vals)
+
+
+# -------------------------------------------------------------- commit ----
+def _check_case(ctx, case, graph=True):
+    import fri_amd
+    st = bytes.fromhex(case["channel_in"]) if case["channel_in"] else None
+    res = ctx.commit(case["coeffs"], case["log_n"], case["offset"], channel_state=st,
+                     forced_betas=case["forced_betas"], graph=graph)
+    assert res.n_layers == len(case["roots"])
+    assert [bytes(res.roots[k]).hex() for k in range(res.n_layers)] == case["roots"]
+    assert [int(res.betas[r]) for r in range(res.n_rounds)] == case["betas"]
+    assert res.final_value == case["final_value"]
+    assert res.final_degree == case["final_degree"]
+    assert bytes(res.channel_out.digest).hex() == case["channel_out"]
+    for k in range(res.n_layers):
+        lay = ctx.layer(k, case["log_n"])
+        assert hashlib.sha256(lay.astype("<u4").tobytes()).hexdigest() == case["layer_sha256"][k]
+    leaves = ctx.tree_level(0, 0, case["log_n"])
+    assert [h.hex() for h in leaves[:4]] == case["leaf0_head"]
+    return fri_amd
+
+
+def test_commit_golden_vectors(ctx, golden):
+    for case in golden["cases"]:
+        _check_case(ctx, case, graph=True)
+
+
+def test_commit_golden_eager(ctx, golden):
+    for case in golden["cases"][::4]:
+        _check_case(ctx, case, graph=False)
+
+
+def test_commit_channel_mirror(ctx, golden, oracle):
+    """fri_commit() drives the host Channel exactly like the reference transcript."""
+    import fri_amd
+    case = [c for c in golden["cases"] if c["name"] == "rand_n9_s42"][0]
+    ch = fri_amd.Channel()
+    proof = fri_amd.fri_commit(case["coeffs"], case["log_n"], ch, ctx=ctx)
+    och = oracle.Channel()
+    oracle.fri_commit(case["coeffs"], case["log_n"], och)
+    assert ch.state == och.state
+    assert ch.proof == och.proof
+    assert ch.proof_size() == case["proof_size"]
+    assert proof.final_poly == [case["final_value"]]
+
+
+@pytest.mark.parametrize("log_n,seed", [(12, 1), (14, 2), (16, 3), (18, 4), (20, 42)])
+def test_commit_matches_fast_oracle(ctx, corc, oracle, log_n, seed):
+    d = (1 << log_n) // 8
+    c = np.array(oracle.splitmix64_field(seed, d), dtype=np.uint64)
+    res = ctx.commit(c, log_n)
+    cs, pc = c_u64(c)
+    och = oracle.OrcChannel()
+    corc.orc_channel_init(ctypes.byref(och))
+    ores = oracle.OrcFriResult()
+    assert corc.orc_fri_commit_fast(pc, d, log_n, 5, 5, P, ctypes.byref(och), None, ctypes.byref(ores),
+                                    None, None) == 0
+    assert res.n_layers == ores.n_layers
+    for k in range(ores.n_layers):
+        assert bytes(res.roots[k]) == bytes(ores.roots[k])
+    for r in range(ores.n_rounds):
+        assert res.betas[r] == ores.betas[r]
+    assert res.final_value == ores.final_value
+    assert bytes(res.channel_out.digest).hex() == och.state.decode()
+
+
+def test_commit_2p24_full_parity(ctx, corc, oracle):
+    """BASELINE config 3 (codeword 2^24, blowup 8): bit-exact against the
+    OpenMP C oracle, plus size-independent properties."""
+    log_n = 24
+    d = 1 << 21
+    c = np.array(oracle.splitmix64_field(42, d), dtype=np.uint64)
+    res = ctx.commit(c, log_n)
+    assert res.n_rounds == 21 and res.n_layers == 22
+    last = ctx.layer(21, log_n)
+    assert last.size == 8 and np.all(last == res.final_value)      # final layer constant
+    cs, pc = c_u64(c)
+    och = oracle.OrcChannel()
+    corc.orc_channel_init(ctypes.byref(och))
+    ores = oracle.OrcFriResult()
+    assert corc.orc_fri_commit_fast(pc, d, log_n, 5, 5, P, ctypes.byref(och), None, ctypes.byref(ores),
+                                    None, None) == 0
+    assert [bytes(res.roots[k]) for k in range(22)] == [bytes(ores.roots[k]) for k in range(22)]
+    assert [res.betas[r] for r in range(21)] == [ores.betas[r] for r in range(21)]
+    assert bytes(res.channel_out.digest).hex() == och.state.decode()
+
+
+def test_auth_path_verifies(ctx, oracle):
+    log_n = 10
+    c = oracle.splitmix64_field(77, 128)
+    res = ctx.commit(c, log_n)
+    for k in (0, 3):
+        for idx in (0, 5, (1 << (log_n - k)) - 1):
+            val, path = ctx.auth_path(k, idx, log_n)
+            h = hashlib.sha256(int(val).to_bytes(8, "big")).digest()
+            i = idx
+            for sib in path:
+                h = hashlib.sha256(h + sib if i % 2 == 0 else sib + h).digest()
+                i //= 2
+            assert h == bytes(res.roots[k])
+
+
+def test_graph_replay_stable(ctx, oracle):
+    c = oracle.splitmix64_field(5, 1 << 13)
+    a = ctx.commit(c, 16)
+    b = ctx.commit(c, 16)
+    c2 = oracle.splitmix64_field(6, 1 << 13)
+    x = ctx.commit(c2, 16)
+    assert bytes(a.roots[0]) == bytes(b.roots[0]) != bytes(x.roots[0])
+    assert [a.betas[i] for i in range(13)] == [b.betas[i] for i in range(13)]
+
+
+def test_error_codes(ctx):
+    import fri_amd
+    with pytest.raises(fri_amd.FriError) as e:
+        ctx.commit([1] * 33, 5)                              # d > n: reference exhausts the domain
+    assert e.value.code == fri_amd.FRI_EDEGREE
+    with pytest.raises(fri_amd.FriError) as e:
+        ctx.commit([P], 5)                                   # not canonical
+    assert e.value.code == fri_amd.FRI_EINVAL
+    with pytest.raises(fri_amd.FriError) as e:
+        ctx.merkle_root([])                                  # merkle/mod.rs:25 unwrap on empty
+    assert e.value.code == fri_amd.FRI_EINVAL
+    with pytest.raises(fri_amd.FriError):
+        ctx.lde([1, 2], 30)                                  # beyond context capacity
