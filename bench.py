@@ -1,0 +1,259 @@
+#!/usr/bin/env python3
+"""bench.py — FRI commit throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--log-n 24]
+
+One step = one full FRI commit (src/fri/fri_commit.rs:72-122) of a synthetic
+random polynomial with d = 2^21 coefficients (blowup 8) onto the codeword
+2^24 = BASELINE.json configs[2]: coset LDE (NTT), 22 SHA-256 Merkle trees
+(all levels kept), 21 Fiat-Shamir rounds and folds, final value — inputs
+resident in HBM when the timed region starts, result (roots, betas, final
+value, channel state) read back to the host at the end of every step.
+
+N > 1 (torchrun, one process per GPU): every rank commits its own 2^24
+codeword (weak scaling; the commit of one codeword is a serial Fiat-Shamir
+chain — see DESIGN.md "Multi-GPU").  value = codeword elements committed per
+second summed over ranks, timed by the slowest rank.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "stark-prover_amd", "python"))
+
+METRIC = "FRI commit field-elems/sec at codeword 2^24; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TOPS = 78.6            # 256 CU x 128 int32 lane-ops/clk x 2.4 GHz
+DOMINANT = "merkle_layer0_leaf"  # dominant kernel class (DESIGN.md "Roofline")
+
+
+def algorithmic_bytes(log_n, d):
+    """B_field = 4d + 8n + 8n, B_tree = 32 * (all tree nodes)."""
+    n = 1 << log_n
+    rounds = max(0, (d - 1).bit_length())
+    rounds = min(rounds, log_n)
+    nodes = sum((2 << (log_n - k)) - 1 for k in range(rounds + 1))
+    layers = sum(1 << (log_n - k) for k in range(rounds + 1))
+    b_field = 4 * d + 4 * layers + 4 * layers
+    return b_field, 32 * nodes
+
+
+def sha_compressions(log_n, d):
+    rounds = min(max(0, (d - 1).bit_length()), log_n)
+    leaves = sum(1 << (log_n - k) for k in range(rounds + 1))
+    nodes = sum((1 << (log_n - k)) - 1 for k in range(rounds + 1))
+    return leaves + 2 * nodes
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=24)
+    ap.add_argument("--blowup-log", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+
+    import numpy as np
+    import fri_amd
+
+    log_n = args.log_n
+    d = 1 << (log_n - args.blowup_log)
+    ctx = fri_amd.Context(local_rank if world > 1 else 0, log_n)
+
+    # synthetic coefficients: splitmix64(seed) % p, seed per rank
+    seed = 42 + rank
+    mask = (1 << 64) - 1
+    x = np.uint64(seed)
+    idx = np.arange(1, d + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + idx * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    coeffs = (z % np.uint64(fri_amd.P)).astype(np.uint32)
+    del x, mask
+
+    # build the plan and place the input in the context's device buffer (untimed)
+    res0 = ctx.commit(coeffs, log_n)
+    dptr = ctypes.c_void_p()
+    ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(dptr)))
+    res = fri_amd.CommitResult()
+
+    def step():
+        rc = ctx.lib.fri_commit_device(ctx.h, dptr, d, log_n, fri_amd.GENERATOR, None, 0, None,
+                                       ctypes.byref(res))
+        ctx._check(rc)
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    assert bytes(res.roots[0]) == bytes(res0.roots[0])
+
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    n = 1 << log_n
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * n * args.steps / elapsed
+
+    # ---- roofline of the dominant kernel: HIP events on the context stream,
+    # recorded around every launch of that kernel during profiled steps.
+    roofline = None
+    breakdown = None
+    if not args.no_profile:
+        ctx.reset_profile()
+        ctx.set_profiling(True)
+        prof_steps = max(3, min(args.steps, 10))
+        for _ in range(prof_steps):
+            step()
+        ctx.set_profiling(False)
+        ms, launches, nbytes = ctx.profile(DOMINANT)
+        if launches:
+            avg_ms = ms / launches
+            per_launch = nbytes / launches
+            achieved = per_launch / (avg_ms * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "kernel": "k_merkle_subtree<LEAF> (layer 0)",
+                        "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                        "bytes_per_launch": per_launch, "avg_launch_ms": round(avg_ms, 4),
+                        "launches": launches}
+            # the honest bound for SHA-256 Merkle work is int32 VALU
+            comp = (1 << log_n) + 2 * ((1 << log_n) - (1 << (log_n - 9)))
+            ops = comp * 1450.0
+            roofline["valu"] = {"sha256_compressions": comp, "est_int32_ops": ops,
+                                "achieved_Tops": round(ops / (avg_ms * 1e-3) / 1e12, 2),
+                                "peak_Tops": VALU_PEAK_TOPS,
+                                "frac": round(ops / (avg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
+        breakdown = {}
+        for cls in ("degree", "lde", "merkle_layer0_leaf", "merkle", "fold", "coeff_fold", "channel"):
+            cms, cl, _ = ctx.profile(cls)
+            if cl:
+                breakdown[cls] = round(cms / prof_steps, 4)
+        traffic = _pmc_traffic(log_n)
+        if roofline is not None and traffic is not None:
+            roofline["traffic"] = traffic
+
+    b_field, b_tree = algorithmic_bytes(log_n, d)
+    whole = {"B_alg_bytes": b_field + b_tree, "B_field_bytes": b_field, "B_tree_bytes": b_tree,
+             "achieved_GBs": round((b_field + b_tree) / (ms_per_step * 1e-3) / 1e9, 2),
+             "frac_of_hbm_peak": round((b_field + b_tree) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+             "sha256_compressions": sha_compressions(log_n, d)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = _cpu_baseline(coeffs, d, log_n)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "field-elems/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (splitmix64 % p coefficients, seed 42+rank)",
+            "config": {"workload": f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} "
+                                   f"(d=2^{log_n - args.blowup_log}), SHA-256 Merkle per layer, "
+                                   f"{res.n_rounds} rounds, per GPU",
+                       "codeword_log2": log_n, "blowup": 1 << args.blowup_log, "field": "p=3*2^30+1",
+                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+            "roofline": roofline,
+            "whole_commit": whole,
+            "breakdown_ms_per_step": breakdown,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _pmc_traffic(log_n):
+    """HBM bytes per launch of the dominant kernel from the committed
+    rocprofv3 PMC summary (profiles/pmc_traffic.json), if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            j = json.load(f)
+        ent = j.get(str(log_n), {}).get(DOMINANT)
+        return ent["hbm_bytes_per_launch"] if ent else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def _cpu_baseline(coeffs, d, log_n):
+    """Oracle timed on the host (checker only, never the product path):
+    the OpenMP C restatement of the same commit (kind "port") at the full
+    2^log_n workload, plus a single-thread faithful-algorithm sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import fri_oracle as fo
+    try:
+        lib = fo.load_c_oracle()
+    except Exception as e:  # noqa: BLE001
+        return {"value": None, "error": f"oracle unavailable: {e}"}
+    c64 = np.ascontiguousarray(coeffs.astype(np.uint64))
+    pc = c64.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    ch = fo.OrcChannel()
+    lib.orc_channel_init(ctypes.byref(ch))
+    r = fo.OrcFriResult()
+    t0 = time.perf_counter()
+    lib.orc_fri_commit_fast(pc, d, log_n, 5, 5, fo.P, ctypes.byref(ch), None, ctypes.byref(r), None, None)
+    t_fast = time.perf_counter() - t0
+    # faithful reference algorithm (Horner LDE, coefficient fold + Horner
+    # re-evaluation), single thread, on a bounded sample codeword 2^13.
+    ls = 13
+    ds = 1 << (ls - 3)
+    cs = np.ascontiguousarray(c64[:ds])
+    pcs = cs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    nthreads = lib.orc_num_threads()
+    lib.orc_set_num_threads(1)
+    ch2 = fo.OrcChannel()
+    lib.orc_channel_init(ctypes.byref(ch2))
+    t0 = time.perf_counter()
+    lib.orc_fri_commit_faithful(pcs, ds, ls, 5, 5, fo.P, ctypes.byref(ch2), None, ctypes.byref(r), None, None)
+    t_faith = time.perf_counter() - t0
+    lib.orc_set_num_threads(nthreads)
+    return {"value": round((1 << log_n) / t_fast, 1), "unit": "field-elems/s", "cores": nthreads,
+            "kind": "port",
+            "sample": f"full workload: OpenMP C restatement (NTT LDE, eval-form fold, SHA-256 Merkle, channel) "
+                      f"at codeword 2^{log_n}, one commit, {t_fast:.2f} s",
+            "faithful_sample": {"value": round((1 << ls) / t_faith, 1), "unit": "field-elems/s", "cores": 1,
+                                "sample": f"reference algorithm (Horner LDE + coefficient fold + Horner "
+                                          f"re-evaluation) at codeword 2^{ls}, d=2^{ls - 3}, {t_faith:.2f} s; "
+                                          f"O(n*d) so 2^24 would be ~{(2**24/2**ls)**2 * t_faith / 86400:.0f} days"}}
+
+
+if __name__ == "__main__":
+    main()

@@ -625,6 +625,14 @@ int orc_fri_commit_fast(const uint64_t* coeffs, size_t d, uint32_t log_n, uint64
     return 0;
 }
 
+void orc_set_num_threads(int n) {
+#ifdef _OPENMP
+    omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
 int orc_num_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

@@ -418,4 +418,6 @@ def load_c_oracle() -> ctypes.CDLL:
     lib.orc_fold_eval.restype = None
     lib.orc_fold_eval.argtypes = [p64, sz, u64, u64, u64, u64, p64]
     lib.orc_num_threads.restype = ctypes.c_int
+    lib.orc_set_num_threads.argtypes = [ctypes.c_int]
+    lib.orc_set_num_threads.restype = None
     return lib
