@@ -146,20 +146,23 @@ def main():
             avg_ms = ms / launches
             per_launch = nbytes / launches
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
-            roofline = {"bound": "hbm", "kernel": "k_merkle_subtree<LEAF> (layer 0)",
+            roofline = {"bound": "hbm", "kernel": "k_layer_leaf (layer 0: leaves + tree levels 1-4)",
                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                         "bytes_per_launch": per_launch, "avg_launch_ms": round(avg_ms, 4),
                         "launches": launches}
-            # the honest bound for SHA-256 Merkle work is int32 VALU
-            comp = (1 << log_n) + 2 * ((1 << log_n) - (1 << (log_n - 9)))
-            ops = comp * 1450.0
-            roofline["valu"] = {"sha256_compressions": comp, "est_int32_ops": ops,
-                                "achieved_Tops": round(ops / (avg_ms * 1e-3) / 1e12, 2),
-                                "peak_Tops": VALU_PEAK_TOPS,
-                                "frac": round(ops / (avg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
+            # The honest bound for SHA-256 Merkle work is int32 VALU issue
+            # (DESIGN.md "VALU cost model"): leaf hash 2009 issue units, node
+            # hash 3592 (v_alignbit/v_add3 are half rate on gfx950).  The leaf
+            # kernel hashes 2^L leaves and (15/16) 2^L nodes (levels 1..4).
+            nleaf = 1 << log_n
+            units = nleaf * 2009.0 + (15.0 / 16.0) * nleaf * 3592.0
+            roofline["valu"] = {"issue_units_per_launch": units,
+                                "achieved_T_units_s": round(units / (avg_ms * 1e-3) / 1e12, 2),
+                                "peak_T_units_s": VALU_PEAK_TOPS,
+                                "frac": round(units / (avg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
         breakdown = {}
-        for cls in ("degree", "lde", "merkle_layer0_leaf", "merkle", "fold", "coeff_fold", "channel"):
+        for cls in ("lde", "merkle_layer0_leaf", "layer0", "layers"):
             cms, cl, _ = ctx.profile(cls)
             if cl:
                 breakdown[cls] = round(cms / prof_steps, 4)

@@ -33,6 +33,7 @@ struct Plan {
     uint32_t* xinv = nullptr;   size_t xinv_off[MAXR + 2] = {0};
     uint32_t* pre_lo = nullptr;
     uint32_t* pre_hi = nullptr;
+    int32_t* wgmax = nullptr;       // per-workgroup coefficient maxima
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     bool graph_profiled = false;
@@ -48,7 +49,7 @@ struct fri_ctx {
     uint32_t log_n_max = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    uint32_t* tw_fwd = nullptr;     // Montgomery w^j, j < 2^(log_n_max-1)
+    uint32_t* tw_fwd = nullptr;     // stage-packed Montgomery twiddles, 2^log_n_max entries
     uint32_t* tw_inv = nullptr;
     uint32_t* scratch_a = nullptr;  // 2^log_n_max words each
     uint32_t* scratch_b = nullptr;
@@ -139,8 +140,8 @@ extern "C" int fri_ctx_create(int device, uint32_t log_n_max, fri_ctx** out) {
     if ((expr) != hipSuccess) { fri_ctx_destroy(ctx); return FRI_ENOMEM; }
     CK(hipSetDevice(device));
     CK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    CK(hipMalloc(&ctx->tw_fwd, (N / 2 + 1) * 4));
-    CK(hipMalloc(&ctx->tw_inv, (N / 2 + 1) * 4));
+    CK(hipMalloc(&ctx->tw_fwd, N * 4));
+    CK(hipMalloc(&ctx->tw_inv, N * 4));
     CK(hipMalloc(&ctx->scratch_a, N * 4));
     CK(hipMalloc(&ctx->scratch_b, N * 4));
     CK(hipMalloc(&ctx->scratch_c, N * 4));
@@ -161,7 +162,7 @@ static void plan_free(fri_ctx* ctx) {
     if (p.exec) hipGraphExecDestroy(p.exec);
     if (p.graph) hipGraphDestroy(p.graph);
     hipFree(p.d_in); hipFree(p.coefA); hipFree(p.coefB); hipFree(p.layers);
-    hipFree(p.trees); hipFree(p.xinv); hipFree(p.pre_lo); hipFree(p.pre_hi);
+    hipFree(p.trees); hipFree(p.xinv); hipFree(p.pre_lo); hipFree(p.pre_hi); hipFree(p.wgmax);
     p = Plan();
 }
 
@@ -205,7 +206,6 @@ static NttPlan lde_plan(fri_ctx* ctx, uint32_t log_n) {
     NttPlan p{};
     p.log_n = log_n;
     p.tw = ctx->tw_fwd;
-    p.log_tw = ctx->log_n_max;
     return p;
 }
 
@@ -242,7 +242,6 @@ extern "C" int fri_interpolate(fri_ctx* ctx, const uint32_t* ys, uint32_t log_n,
     NttPlan p{};
     p.log_n = log_n;
     p.tw = ctx->tw_inv;
-    p.log_tw = ctx->log_n_max;
     // coeff_j = n^-1 * offset^-j * sum_i ys_i w^-ij
     launch_pow_table(ctx->pow_lo, ctx->pow_hi, log_n, inv_std(offset), inv_std((uint32_t)(n % P)), ctx->stream);
     p.post_lo = ctx->pow_lo;
@@ -327,7 +326,11 @@ extern "C" int fri_merkle_root(fri_ctx* ctx, const uint32_t* values, size_t n, u
         uint32_t L = 0;
         while (((size_t)1 << L) < n) L++;
         FRI_HIP(ctx, hipMalloc(&tree, (((size_t)2 << L)) * 32));
-        launch_merkle_tree(ctx->scratch_a, tree, L, nullptr, -1, ctx->stream);
+        LayerTask t{};
+        t.values = ctx->scratch_a;
+        t.tree = tree;
+        t.L = L;
+        launch_layer(t, ctx->stream);
         root_dev = tree + 8 * level_offset(L, L);
     } else {
         size_t total = 0;
@@ -394,7 +397,8 @@ static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset) {
         hipMalloc(&p.coefB, p.coef_cap * 4) != hipSuccess || hipMalloc(&p.layers, lay * 4) != hipSuccess ||
         hipMalloc(&p.trees, tre * 4) != hipSuccess || hipMalloc(&p.xinv, (xin ? xin : 1) * 4) != hipSuccess ||
         hipMalloc(&p.pre_lo, ((size_t)1 << POW_LO_LOG) * 4) != hipSuccess ||
-        hipMalloc(&p.pre_hi, nhi * 4) != hipSuccess) {
+        hipMalloc(&p.pre_hi, nhi * 4) != hipSuccess ||
+        hipMalloc(&p.wgmax, 3 * ((log_n > 10 ? ((size_t)1 << (log_n - 10)) : 1) + 1) * 4) != hipSuccess) {
         plan_free(ctx);
         return fail(ctx, FRI_ENOMEM, "device allocation failed for commit plan");
     }
@@ -419,56 +423,48 @@ static const uint32_t* root_ptr(const Plan& p, int k) {
     return p.trees + p.tree_off[k] + 8 * level_offset(L, L);
 }
 
-// Enqueue the whole commit on ctx->stream (captured into a graph or eager).
+// poly_r coefficient buffer: poly_0 is the input, then A/B alternate.
+static uint32_t* coef_buf(Plan& p, int r) {
+    if (r == 0) return p.d_in;
+    return (r % 2 == 1) ? p.coefA : p.coefB;
+}
+
+// Enqueue the whole commit on ctx->stream (captured into a graph or eager):
+// LDE, then per layer k = 0..rmax one launch_layer (gated on the device).
 static void enqueue_commit(fri_ctx* ctx) {
     Plan& p = ctx->plan;
     hipStream_t s = ctx->stream;
     const uint32_t log_n = p.log_n;
     const size_t n = (size_t)1 << log_n;
-    size_t sp;
-    sp = span_begin(ctx, "degree", p.d * 4);
-    launch_degree0(p.d_in, p.d, ctx->d_state, s);
-    span_end(ctx, sp);
     NttPlan np = lde_plan(ctx, log_n);
     np.pre_lo = p.pre_lo;
     np.pre_hi = p.pre_hi;
-    sp = span_begin(ctx, "lde", p.d * 4 + n * 4);
+    size_t sp = span_begin(ctx, "lde", p.d * 4 + n * 4);
     launch_ntt(np, p.d_in, p.d, p.layers + p.layer_off[0], s);
     span_end(ctx, sp);
-    // Algorithmic bytes of a merkle_leaf launch over 2^L values: read 4 B per
-    // value, write every digest of the levels it builds (32 B each).
-    auto tree_bytes = [](uint32_t L) -> uint64_t {
-        uint32_t h = L < SUBTREE_LOG ? L : SUBTREE_LOG;
-        uint64_t nodes = 0;
-        for (uint32_t j = 0; j <= h; j++) nodes += (uint64_t)1 << (L - j);
-        return ((uint64_t)4 << L) + 32 * nodes;
-    };
-    // Layer-0 tree: the leaf kernel (dominant kernel of the commit) is timed
-    // on its own; its span ends right after the leaf launch.
-    size_t spl = span_begin(ctx, "merkle_layer0_leaf", tree_bytes(log_n));
-    launch_merkle_tree(p.layers + p.layer_off[0], p.trees + p.tree_off[0], log_n, ctx->d_state, -1, s, nullptr,
-                       spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
-    sp = span_begin(ctx, "channel", 0);
-    launch_channel_step(ctx->d_state, 0, p.d_in, root_ptr(p, 0), log_n, s);
-    span_end(ctx, sp);
-    for (int r = 0; r < p.rmax; r++) {
-        uint32_t L = log_n - (uint32_t)r;
-        sp = span_begin(ctx, "fold", ((uint64_t)4 << L) + ((uint64_t)2 << L) + ((uint64_t)2 << L));
-        launch_fold_round(p.layers + p.layer_off[r], p.layers + p.layer_off[r + 1], L, p.xinv + p.xinv_off[r],
-                          ctx->d_state, r, s);
-        span_end(ctx, sp);
-        const uint32_t* csrc = (r == 0) ? p.d_in : ((r - 1) % 2 == 0 ? p.coefA : p.coefB);
-        uint32_t* cdst = (r % 2 == 0) ? p.coefA : p.coefB;
-        size_t cap = (p.d + ((size_t)2 << r) - 1) >> (r + 1);
-        sp = span_begin(ctx, "coeff_fold", cap * 12);
-        launch_coeff_fold(csrc, cdst, cap, ctx->d_state, r, s);
-        span_end(ctx, sp);
-        sp = span_begin(ctx, "merkle", tree_bytes(L - 1));
-        launch_merkle_tree(p.layers + p.layer_off[r + 1], p.trees + p.tree_off[r + 1], L - 1, ctx->d_state, r, s);
-        span_end(ctx, sp);
-        sp = span_begin(ctx, "channel", 0);
-        launch_channel_step(ctx->d_state, r + 1, cdst, root_ptr(p, r + 1), L - 1, s);
-        span_end(ctx, sp);
+    for (int k = 0; k <= p.rmax; k++) {
+        const uint32_t L = log_n - (uint32_t)k;
+        LayerTask t{};
+        t.prev = k ? p.layers + p.layer_off[k - 1] : nullptr;
+        t.xinv = k ? p.xinv + p.xinv_off[k - 1] : nullptr;
+        t.values = p.layers + p.layer_off[k];
+        t.tree = p.trees + p.tree_off[k];
+        t.L = L;
+        t.k = k;
+        t.coef_in = k ? coef_buf(p, k - 1) : p.d_in;
+        t.coef_out = k ? coef_buf(p, k) : nullptr;
+        t.d0 = p.d;
+        t.wgmax = p.wgmax;
+        t.st = ctx->d_state;
+        // Algorithmic bytes of layer 0's leaf kernel: read the values and the
+        // input coefficients (degree scan), write tree levels 0..4.
+        uint64_t leaf_nodes = 0;
+        for (uint32_t j = 0; j <= 4 && j <= L; j++) leaf_nodes += (uint64_t)1 << (L - j);
+        const uint64_t leaf_bytes = ((uint64_t)4 << L) + 4 * (uint64_t)p.d + 32 * leaf_nodes;
+        size_t spl = (k == 0 && L > TOP_LOG) ? span_begin(ctx, "merkle_layer0_leaf", leaf_bytes) : (size_t)-1;
+        size_t spk = span_begin(ctx, k == 0 ? "layer0" : "layers", 0);
+        launch_layer(t, s, spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
+        span_end(ctx, spk);
     }
 }
 

@@ -12,7 +12,7 @@ constexpr int MAXR = 32;            // == FRI_MAX_ROUNDS
 constexpr uint32_t NTT_TILE_LOG = 12;   // first-pass LDS tile: 4096 elements
 constexpr uint32_t NTT_MID_LOG = 10;    // middle-pass stages per launch
 constexpr uint32_t NTT_MID_W = 16;      // middle-pass contiguous run (64 B)
-constexpr uint32_t SUBTREE_LOG = 9;     // Merkle subtree per workgroup: 512 items (1 node per lane per level)
+constexpr uint32_t TOP_LOG = 10;        // single-workgroup tree top: <= 1024 inputs
 constexpr uint32_t POW_LO_LOG = 12;     // two-level power tables s^j = lo[j&4095]*hi[j>>12]
 
 // Device-resident commit state (one per context).  Every per-round kernel
@@ -49,8 +49,7 @@ __host__ __device__ inline size_t level_offset(uint32_t L, uint32_t l) {
 // ---- launchers (fri_kernels.hip); all asynchronous on `s` ----------------
 struct NttPlan {
     uint32_t log_n;              // transform size 2^log_n
-    const uint32_t* tw;          // Montgomery twiddles w_{2^log_tw}^j, j < 2^(log_tw-1)
-    uint32_t log_tw;
+    const uint32_t* tw;          // stage-packed Montgomery twiddles: tw[2^s + j] = w_{2^(s+1)}^j
     const uint32_t* pre_lo;      // optional input scale s^j (Montgomery, two-level)
     const uint32_t* pre_hi;
     const uint32_t* post_lo;     // optional output scale t^j (Montgomery, two-level)
@@ -59,7 +58,8 @@ struct NttPlan {
 // dst[k] = post(k) * sum_{j<d} src[j]*pre(j)*w^(jk); src may alias nothing in dst.
 void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, hipStream_t s);
 
-void launch_twiddles(uint32_t* tw, uint32_t log_tw, bool inverse, hipStream_t s);
+// tw[2^s + j] = Montgomery(w_{2^(s+1)}^{+-j}), s < log_max, j < 2^s (2^log_max entries)
+void launch_twiddles(uint32_t* tw, uint32_t log_max, bool inverse, hipStream_t s);
 void launch_pow_table(uint32_t* lo, uint32_t* hi, uint32_t log_n, uint32_t base_std,
                       uint32_t scale_std, hipStream_t s);
 void launch_batch_inverse(const uint32_t* in, uint32_t* out, size_t n, int out_mont,
@@ -72,18 +72,23 @@ void launch_evaluate(const uint32_t* coeffs, size_t d, const uint32_t* xs, size_
 void launch_fold_plain(const uint32_t* in, uint32_t* out, uint32_t log_m, const uint32_t* xinv_m,
                        uint32_t beta, hipStream_t s);
 
-// Merkle: hash layer (2^L values) into its tree (all levels).
-void launch_merkle_tree(const uint32_t* values, uint32_t* tree, uint32_t L,
-                        const DevState* st, int gate_round, hipStream_t s,
-                        hipEvent_t ev_leaf_begin = nullptr, hipEvent_t ev_leaf_end = nullptr);
-
-// Commit-path kernels gated on st->active[r].
-void launch_degree0(const uint32_t* coeffs, size_t d, DevState* st, hipStream_t s);
-void launch_fold_round(const uint32_t* in, uint32_t* out, uint32_t log_m, const uint32_t* xinv_m,
-                       const DevState* st, int r, hipStream_t s);
-void launch_coeff_fold(const uint32_t* c, uint32_t* cn, size_t cap, DevState* st, int r,
-                       hipStream_t s);
-void launch_channel_step(DevState* st, int k, const uint32_t* coef_k, const uint32_t* root,
-                         uint32_t log_n_k, hipStream_t s);
+// One FRI layer (fri_layer.hip): optional fold of the previous layer, leaf
+// hashes, every tree level, and (commit mode, st != nullptr) the coefficient
+// fold slice, degree resolution and Fiat-Shamir step of layer k.
+struct LayerTask {
+    const uint32_t* prev;      // layer k-1 values (fold) or nullptr
+    const uint32_t* xinv;      // Montgomery (x_i)^-1 of layer k-1's domain, i < 2^L
+    uint32_t* values;          // layer k values (written when folding)
+    uint32_t* tree;            // layer k tree: levels 0..L (level_offset)
+    uint32_t L;                // log2 |layer k|
+    int k;                     // layer index (commit mode)
+    uint32_t beta_m;           // Montgomery beta for a standalone fold (no state)
+    const uint32_t* coef_in;   // k == 0: input coefficients; else poly_{k-1}
+    uint32_t* coef_out;        // poly_k coefficients (k >= 1)
+    size_t d0;                 // k == 0: input length
+    int32_t* wgmax;            // [3 * workgroups] coefficient maxima
+    DevState* st;              // nullptr: standalone Merkle tree
+};
+void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end = nullptr);
 
 }  // namespace fri

@@ -32,14 +32,16 @@ __device__ __forceinline__ uint32_t pow2lvl(const uint32_t* lo, const uint32_t* 
 
 __global__ __launch_bounds__(256) void k_ntt_first(const uint32_t* __restrict__ src, size_t d,
                                                    uint32_t* __restrict__ dst, uint32_t log_n, uint32_t tb,
-                                                   const uint32_t* __restrict__ tw, uint32_t log_tw,
+                                                   const uint32_t* __restrict__ tw,
                                                    const uint32_t* __restrict__ pre_lo,
                                                    const uint32_t* __restrict__ pre_hi,
                                                    const uint32_t* __restrict__ post_lo,
                                                    const uint32_t* __restrict__ post_hi) {
     __shared__ uint32_t lds[1u << NTT_TILE_LOG];
+    __shared__ uint32_t twl[1u << NTT_TILE_LOG];
     const uint32_t T = 1u << tb;
     const size_t base = (size_t)blockIdx.x << tb;
+    for (uint32_t i = threadIdx.x; i < T; i += blockDim.x) twl[i] = tw[i];
     for (uint32_t i = threadIdx.x; i < T; i += blockDim.x) {
         uint32_t pos = (uint32_t)(base + i);
         uint32_t si = log_n ? (__brev(pos) >> (32 - log_n)) : 0u;
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(256) void k_ntt_first(const uint32_t* __restrict__ 
         for (uint32_t b = threadIdx.x; b < T / 2; b += blockDim.x) {
             uint32_t j = b & (h - 1);
             uint32_t i0 = ((b >> s) << (s + 1)) + j, i1 = i0 + h;
-            uint32_t w = tw[(size_t)j << (log_tw - 1 - s)];
+            uint32_t w = twl[h + j];
             uint32_t u = lds[i0], v = mmul(lds[i1], w);
             lds[i0] = add(u, v);
             lds[i1] = sub(u, v);
@@ -71,7 +73,7 @@ __global__ __launch_bounds__(256) void k_ntt_first(const uint32_t* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void k_ntt_mid(uint32_t* __restrict__ data, uint32_t log_n, uint32_t s0,
-                                                 uint32_t ns, const uint32_t* __restrict__ tw, uint32_t log_tw,
+                                                 uint32_t ns, const uint32_t* __restrict__ tw,
                                                  const uint32_t* __restrict__ post_lo,
                                                  const uint32_t* __restrict__ post_hi) {
     __shared__ uint32_t lds[NTT_MID_W << NTT_MID_LOG];
@@ -91,7 +93,7 @@ __global__ __launch_bounds__(256) void k_ntt_mid(uint32_t* __restrict__ data, ui
             uint32_t jm = bm & (hm - 1);
             uint32_t m0 = ((bm >> t) << (t + 1)) + jm, m1 = m0 + hm;
             uint32_t j = lo0 + lo + (jm << s0);
-            uint32_t w = tw[(size_t)j << (log_tw - 1 - s)];
+            uint32_t w = tw[((size_t)1 << s) + j];
             uint32_t u = lds[m0 * W + lo], v = mmul(lds[m1 * W + lo], w);
             lds[m0 * W + lo] = add(u, v);
             lds[m1 * W + lo] = sub(u, v);
@@ -112,28 +114,36 @@ void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, 
     const uint32_t tb = log_n < NTT_TILE_LOG ? log_n : NTT_TILE_LOG;
     const bool single = (tb == log_n);
     const uint32_t nblk = 1u << (log_n - tb);
-    hipLaunchKernelGGL(k_ntt_first, dim3(nblk), dim3(256), 0, s, src, d, dst, log_n, tb, p.tw, p.log_tw,
+    hipLaunchKernelGGL(k_ntt_first, dim3(nblk), dim3(256), 0, s, src, d, dst, log_n, tb, p.tw,
                        p.pre_lo, p.pre_hi, single ? p.post_lo : nullptr, single ? p.post_hi : nullptr);
     for (uint32_t s0 = tb; s0 < log_n;) {
         uint32_t ns = (log_n - s0) < NTT_MID_LOG ? (log_n - s0) : NTT_MID_LOG;
         bool last = (s0 + ns == log_n);
         uint32_t blocks = (uint32_t)(((size_t)1 << log_n) / ((size_t)NTT_MID_W << ns));
-        hipLaunchKernelGGL(k_ntt_mid, dim3(blocks), dim3(256), 0, s, dst, log_n, s0, ns, p.tw, p.log_tw,
+        hipLaunchKernelGGL(k_ntt_mid, dim3(blocks), dim3(256), 0, s, dst, log_n, s0, ns, p.tw,
                            last ? p.post_lo : nullptr, last ? p.post_hi : nullptr);
         s0 += ns;
     }
 }
 
-// tw[j] = Montgomery(w^j), j < 2^(log_tw-1), w = primitive 2^log_tw-th root (or its inverse).
-__global__ void k_twiddles(uint32_t* tw, size_t count, uint32_t w_m) {
-    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < count) tw[j] = mpow(w_m, j);
+// Stage-packed twiddles: tw[2^s + j] = Montgomery(w_{2^(s+1)}^j), so every
+// DIT stage s reads a contiguous run (independent of the transform size).
+struct StageBases { uint32_t b[32]; };
+__global__ void k_twiddles(uint32_t* tw, size_t count, StageBases sb) {
+    size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= count) return;
+    if (e == 0) { tw[0] = R_MOD_P; return; }
+    uint32_t s = 63u - (uint32_t)__clzll((unsigned long long)e);
+    tw[e] = mpow(sb.b[s], e - ((size_t)1 << s));
 }
-void launch_twiddles(uint32_t* tw, uint32_t log_tw, bool inverse, hipStream_t s) {
-    uint32_t w = root_of_unity(log_tw);
-    if (inverse) w = inv_std(w);
-    size_t count = log_tw ? ((size_t)1 << (log_tw - 1)) : 1;
-    hipLaunchKernelGGL(k_twiddles, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, tw, count, to_mont(w));
+void launch_twiddles(uint32_t* tw, uint32_t log_max, bool inverse, hipStream_t s) {
+    StageBases sb{};
+    for (uint32_t st = 0; st < log_max && st < 31; st++) {
+        uint32_t w = root_of_unity(st + 1);
+        sb.b[st] = to_mont(inverse ? inv_std(w) : w);
+    }
+    size_t count = (size_t)1 << log_max;
+    hipLaunchKernelGGL(k_twiddles, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, tw, count, sb);
 }
 
 // Two-level power table of base^j scaled by `scale`: lo[t] = base^t,
@@ -249,204 +259,6 @@ void launch_fold_plain(const uint32_t* in, uint32_t* out, uint32_t log_m, const 
     size_t half = ((size_t)1 << log_m) / 2;
     hipLaunchKernelGGL(k_fold, dim3((unsigned)((half + 255) / 256)), dim3(256), 0, s, in, out, half, xinv_m,
                        to_mont(beta), (const DevState*)nullptr, 0);
-}
-void launch_fold_round(const uint32_t* in, uint32_t* out, uint32_t log_m, const uint32_t* xinv_m,
-                       const DevState* st, int r, hipStream_t s) {
-    size_t half = ((size_t)1 << log_m) / 2;
-    hipLaunchKernelGGL(k_fold, dim3((unsigned)((half + 255) / 256)), dim3(256), 0, s, in, out, half, xinv_m, 0u, st,
-                       r);
-}
-
-// ======================================================= degree tracking ==
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-    return v;
-}
-
-__global__ __launch_bounds__(256) void k_degree0(const uint32_t* __restrict__ c, size_t d, DevState* st) {
-    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int m = (j < d && c[j] != 0) ? (int)j : -1;
-    m = wave_max(m);
-    if ((threadIdx.x & 63) == 0 && m >= 0) atomicMax(&st->deg0max, m);
-}
-void launch_degree0(const uint32_t* coeffs, size_t d, DevState* st, hipStream_t s) {
-    if (!d) return;
-    hipLaunchKernelGGL(k_degree0, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, coeffs, d, st);
-}
-
-// next_fri_polynomial (fri_commit.rs:32-50): c'_j = c_2j + beta*c_2j+1 for
-// j < ceil(len/2), len = deg_r + 1, plus the three maxima that reproduce the
-// reference's degree field exactly (channel step resolves them).
-__global__ __launch_bounds__(256) void k_coeff_fold(const uint32_t* __restrict__ c, uint32_t* __restrict__ cn,
-                                                    size_t cap, DevState* st, int r) {
-    if (!st->active[r]) return;
-    const size_t len = (size_t)(st->deg[r] + 1);
-    const size_t nlen = (len + 1) / 2;
-    const uint32_t beta_m = st->beta_mont[r];
-    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int nm = -1, em = -1, om = -1;
-    if (j < nlen && j < cap) {
-        uint32_t e = c[2 * j];
-        uint32_t o = (2 * j + 1 < len) ? c[2 * j + 1] : 0u;
-        uint32_t v = add(e, mmul(o, beta_m));
-        cn[j] = v;
-        nm = v ? (int)j : -1;
-        em = e ? (int)j : -1;
-        om = o ? (int)j : -1;
-    }
-    nm = wave_max(nm); em = wave_max(em); om = wave_max(om);
-    if ((threadIdx.x & 63) == 0) {
-        if (nm >= 0) atomicMax(&st->newmax[r], nm);
-        if (em >= 0) atomicMax(&st->evenmax[r], em);
-        if (om >= 0) atomicMax(&st->oddmax[r], om);
-    }
-}
-void launch_coeff_fold(const uint32_t* c, uint32_t* cn, size_t cap, DevState* st, int r, hipStream_t s) {
-    if (!cap) return;
-    hipLaunchKernelGGL(k_coeff_fold, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, c, cn, cap, st, r);
-}
-
-// ================================================================ Merkle ==
-// One workgroup builds a subtree of height h (<= 9) over 2^h consecutive
-// items of level l0 — leaf hashes of layer values (LEAF) or stored digests —
-// writing every level it produces.  Leaf digests go straight to HBM with
-// lane-contiguous 32-byte stores; upper levels are paired through LDS.
-template <bool LEAF>
-__global__ __launch_bounds__(256) void k_merkle_subtree(const uint32_t* __restrict__ values, uint32_t* __restrict__ tree,
-                                                        uint32_t L, uint32_t l0, uint32_t h,
-                                                        const DevState* __restrict__ st, int gate) {
-    if (gate >= 0 && !st->active[gate]) return;
-    __shared__ uint4 lds[2u << SUBTREE_LOG];
-    const uint32_t S = 1u << h;
-    const size_t wbase = (size_t)blockIdx.x << h;
-    uint4* lvl0 = reinterpret_cast<uint4*>(tree + 8 * level_offset(L, l0));
-#pragma unroll 1
-    for (uint32_t i = threadIdx.x; i < S; i += blockDim.x) {
-        uint4 d0, d1;
-        if (LEAF) {
-            uint32_t dg[8];
-            sha::leaf(values[wbase + i], dg);
-            d0 = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-            d1 = make_uint4(dg[4], dg[5], dg[6], dg[7]);
-            lvl0[2 * (wbase + i)] = d0;
-            lvl0[2 * (wbase + i) + 1] = d1;
-        } else {
-            d0 = lvl0[2 * (wbase + i)];
-            d1 = lvl0[2 * (wbase + i) + 1];
-        }
-        lds[2 * i] = d0;
-        lds[2 * i + 1] = d1;
-    }
-    __syncthreads();
-    for (uint32_t j = 1; j <= h; j++) {
-        const uint32_t cnt = S >> j;
-        const uint32_t q = threadIdx.x;
-        uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0;
-        if (q < cnt) {
-            uint4 a0 = lds[4 * q], a1 = lds[4 * q + 1], b0 = lds[4 * q + 2], b1 = lds[4 * q + 3];
-            uint32_t l[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            uint32_t rr[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-            uint32_t o[8];
-            sha::node(l, rr, o);
-            r0 = make_uint4(o[0], o[1], o[2], o[3]);
-            r1 = make_uint4(o[4], o[5], o[6], o[7]);
-        }
-        __syncthreads();
-        if (q < cnt) {
-            lds[2 * q] = r0;
-            lds[2 * q + 1] = r1;
-            uint4* lvl = reinterpret_cast<uint4*>(tree + 8 * level_offset(L, l0 + j));
-            size_t gi = (wbase >> j) + q;
-            lvl[2 * gi] = r0;
-            lvl[2 * gi + 1] = r1;
-        }
-        __syncthreads();
-    }
-}
-
-void launch_merkle_tree(const uint32_t* values, uint32_t* tree, uint32_t L, const DevState* st, int gate,
-                        hipStream_t s, hipEvent_t ev_b, hipEvent_t ev_e) {
-    uint32_t h = L < SUBTREE_LOG ? L : SUBTREE_LOG;
-    if (ev_b) hipEventRecord(ev_b, s);
-    hipLaunchKernelGGL(k_merkle_subtree<true>, dim3(1u << (L - h)), dim3(256), 0, s, values, tree, L, 0u, h, st,
-                       gate);
-    if (ev_e) hipEventRecord(ev_e, s);
-    for (uint32_t l = h; l < L;) {
-        uint32_t hh = (L - l) < SUBTREE_LOG ? (L - l) : SUBTREE_LOG;
-        hipLaunchKernelGGL(k_merkle_subtree<false>, dim3(1u << (L - l - hh)), dim3(256), 0, s, values, tree, L, l,
-                           hh, st, gate);
-        l += hh;
-    }
-}
-
-// =============================================================== channel ==
-// Single-lane Fiat-Shamir step for committed layer k (frozen spec):
-//   send(root_hex.as_bytes()):  state = sha256_hex(state || hex(root_hex))
-//   if deg_k >= 1: beta = U256(state) mod p; state = sha256_hex(state)
-//   else:          send(final.to_bytes())
-__device__ void chan_send(DevState* st, const uint8_t* msg, uint32_t len) {
-    uint8_t buf[256];
-    uint32_t n = 0;
-    if (st->chan_has) {
-        char hx[64];
-        sha::digest_hex(st->chan, hx);
-        for (int i = 0; i < 64; i++) buf[n++] = (uint8_t)hx[i];
-    }
-    for (uint32_t i = 0; i < len; i++) {
-        buf[n++] = (uint8_t)sha::hexc(msg[i] >> 4);
-        buf[n++] = (uint8_t)sha::hexc(msg[i] & 15u);
-    }
-    uint32_t out[8];
-    sha::bytes(buf, n, out);
-    for (int i = 0; i < 8; i++) st->chan[i] = out[i];
-    st->chan_has = 1;
-}
-
-__device__ uint32_t chan_receive_fe(DevState* st) {
-    uint64_t r = 0;
-    for (int i = 0; i < 8; i++) r = ((r << 32) | st->chan[i]) % P;        // channel.rs:64-72
-    char hx[64];
-    sha::digest_hex(st->chan, hx);
-    uint32_t out[8];
-    sha::bytes(reinterpret_cast<const uint8_t*>(hx), 64, out);             // channel.rs:75-76
-    for (int i = 0; i < 8; i++) st->chan[i] = out[i];
-    return (uint32_t)r;
-}
-
-__global__ void k_channel_step(DevState* st, int k, const uint32_t* __restrict__ coef_k,
-                               const uint32_t* __restrict__ root, uint32_t log_n_k) {
-    if (threadIdx.x != 0) return;
-    if (k > 0 && !st->active[k - 1]) return;
-    int deg;
-    if (k == 0) deg = st->deg0max;
-    else deg = (st->evenmax[k - 1] < 0) ? st->oddmax[k - 1] : st->newmax[k - 1];
-    st->deg[k] = deg;
-    for (int i = 0; i < 8; i++) st->roots[k][i] = root[i];
-    char hx[64];
-    sha::digest_hex(root, hx);
-    chan_send(st, reinterpret_cast<const uint8_t*>(hx), 64);
-    st->n_layers = (uint32_t)k + 1;
-    if (deg >= 1 && k < MAXR && log_n_k >= 1) {
-        uint32_t beta = chan_receive_fe(st);
-        if (st->forced) beta = st->forced_beta[k];
-        st->beta[k] = beta;
-        st->beta_mont[k] = to_mont(beta);
-        st->active[k] = 1;
-        st->n_rounds = (uint32_t)k + 1;
-    } else {
-        st->active[k] = 0;
-        if (deg >= 1) { st->status = 7u; return; }                  // FRI_EDEGREE
-        uint32_t fv = (deg == -1) ? 0u : coef_k[0];
-        st->final_value = fv;
-        st->final_degree = deg;
-        uint8_t be[8] = {0, 0, 0, 0, (uint8_t)(fv >> 24), (uint8_t)(fv >> 16), (uint8_t)(fv >> 8), (uint8_t)fv};
-        chan_send(st, be, 8);
-    }
-}
-void launch_channel_step(DevState* st, int k, const uint32_t* coef_k, const uint32_t* root, uint32_t log_n_k,
-                         hipStream_t s) {
-    hipLaunchKernelGGL(k_channel_step, dim3(1), dim3(64), 0, s, st, k, coef_k, root, log_n_k);
 }
 
 }  // namespace fri

@@ -1,0 +1,384 @@
+// fri_layer.hip — per-layer FRI commit pipeline on gfx950.
+//
+// One FRI layer k (2^L evaluations) is committed by at most three kinds of
+// launch, all gated on the device state (no host round trip per round):
+//
+//   k_layer_leaf  (2^(L-10) workgroups, L >= 11)
+//       fold of layer k-1 with beta_{k-1}      (src/fri/fri_commit.rs:53-65)
+//       leaf hashes SHA256(u64_be(v))           (src/merkle/mod.rs:14-15)
+//       tree levels 1..4 (1024 leaves -> 64 nodes per workgroup)
+//       a slice of the coefficient fold of round k-1 (fri_commit.rs:32-50)
+//       with per-workgroup maxima (no hot atomics) for the exact degree
+//   k_tree_mid    (levels l -> l+4, 1024 nodes in / 64 out per workgroup)
+//   k_tree_top    (ONE workgroup): last <= 10 levels -> root, degree of
+//       poly_k, Fiat-Shamir step (channel.rs:35-55): send(root_hex),
+//       beta_k = U256(state) mod p or the final send (fri_commit.rs:114).
+//       For layers of <= 2^10 elements it also does the fold, the leaves and
+//       the whole coefficient fold itself (single launch per small layer).
+//
+// Each thread of the leaf / mid kernels takes 4 consecutive inputs and folds
+// them to one level+2 node in registers (no LDS, no barrier, no idle lanes);
+// levels +3/+4 pair through LDS.  Loads/stores of values are 16 B per lane.
+#include "fri_internal.hpp"
+#include "sha256_fast.hpp"
+
+namespace fri {
+
+constexpr uint32_t INV2_M2 = 0x80000000u;   // Montgomery(2^-1) = 2^31 mod p
+
+__device__ __forceinline__ uint32_t fold1(uint32_t a, uint32_t b, uint32_t xinv_m, uint32_t beta_m) {
+    uint32_t s = add(a, b), t = sub(a, b);
+    return mmul(add(s, mmul(mmul(t, xinv_m), beta_m)), INV2_M2);
+}
+
+struct Dg { uint32_t w[8]; };
+
+__device__ __forceinline__ void dg_load(const uint32_t* p, Dg& d) {
+    uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+    d.w[0] = a.x; d.w[1] = a.y; d.w[2] = a.z; d.w[3] = a.w; d.w[4] = b.x; d.w[5] = b.y; d.w[6] = b.z; d.w[7] = b.w;
+}
+__device__ __forceinline__ void dg_store(uint32_t* p, const Dg& d) {
+    reinterpret_cast<uint4*>(p)[0] = make_uint4(d.w[0], d.w[1], d.w[2], d.w[3]);
+    reinterpret_cast<uint4*>(p)[1] = make_uint4(d.w[4], d.w[5], d.w[6], d.w[7]);
+}
+__device__ __forceinline__ void dg_lds_load(const uint4* p, Dg& d) {
+    uint4 a = p[0], b = p[1];
+    d.w[0] = a.x; d.w[1] = a.y; d.w[2] = a.z; d.w[3] = a.w; d.w[4] = b.x; d.w[5] = b.y; d.w[6] = b.z; d.w[7] = b.w;
+}
+__device__ __forceinline__ void dg_lds_store(uint4* p, const Dg& d) {
+    p[0] = make_uint4(d.w[0], d.w[1], d.w[2], d.w[3]);
+    p[1] = make_uint4(d.w[4], d.w[5], d.w[6], d.w[7]);
+}
+__device__ __forceinline__ void hnode(const Dg& l, const Dg& r, Dg& o) { shaf::node(l.w, r.w, o.w); }
+__device__ __forceinline__ void hleaf(uint32_t v, Dg& o) { shaf::leaf(v, o.w); }
+
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
+    return v;
+}
+
+// Coefficient task of one workgroup (w of G): k == 0 -> max nonzero index
+// of the input (deg_0); k >= 1 -> fold slice c'_j = c_2j + beta c_2j+1 with
+// maxima of c', even part, odd part.  Results: wgmax[3w .. 3w+2].
+__device__ void coef_task(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red /*LDS [3*4]*/) {
+    int m0 = -1, m1 = -1, m2 = -1;
+    if (t.k == 0) {
+        const size_t n = t.d0, cs = (n + G - 1) / G, lo = (size_t)w * cs, hi = min(n, lo + cs);
+        for (size_t j = lo + threadIdx.x; j < hi; j += blockDim.x)
+            if (t.coef_in[j]) m0 = max(m0, (int)j);
+    } else {
+        const DevState* st = t.st;
+        const size_t len = (size_t)(st->deg[t.k - 1] + 1), nlen = (len + 1) / 2;
+        const uint32_t beta_m = st->beta_mont[t.k - 1];
+        const size_t cs = (nlen + G - 1) / G, lo = (size_t)w * cs, hi = min(nlen, lo + cs);
+        for (size_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+            uint32_t e = t.coef_in[2 * j];
+            uint32_t o = (2 * j + 1 < len) ? t.coef_in[2 * j + 1] : 0u;
+            uint32_t v = add(e, mmul(o, beta_m));
+            t.coef_out[j] = v;
+            if (v) m0 = (int)j;
+            if (e) m1 = (int)j;
+            if (o) m2 = (int)j;
+        }
+    }
+    m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
+    const uint32_t wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[3 * wave] = m0; red[3 * wave + 1] = m1; red[3 * wave + 2] = m2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int a = -1, b = -1, c = -1;
+        for (uint32_t i = 0; i < blockDim.x / 64; i++) { a = max(a, red[3 * i]); b = max(b, red[3 * i + 1]); c = max(c, red[3 * i + 2]); }
+        t.wgmax[3 * w] = a; t.wgmax[3 * w + 1] = b; t.wgmax[3 * w + 2] = c;
+    }
+}
+
+// Four consecutive level-l digests (or leaves) per thread -> level l+2 node.
+// lv0/lv1 are this layer's level l+0 / l+1 arrays (lv0 written only for
+// leaves: it is the input otherwise).
+template <bool LEAVES>
+__device__ __forceinline__ void quad(const uint4& vals, const uint32_t* in0, uint32_t* lv0, uint32_t* lv1,
+                                     size_t q /*quad index*/, Dg& out) {
+    Dg a, b, n0, n1;
+    if (LEAVES) { hleaf(vals.x, a); hleaf(vals.y, b); dg_store(lv0 + 8 * (4 * q), a); dg_store(lv0 + 8 * (4 * q + 1), b); }
+    else { dg_load(in0 + 8 * (4 * q), a); dg_load(in0 + 8 * (4 * q + 1), b); }
+    hnode(a, b, n0);
+    dg_store(lv1 + 8 * (2 * q), n0);
+    if (LEAVES) { hleaf(vals.z, a); hleaf(vals.w, b); dg_store(lv0 + 8 * (4 * q + 2), a); dg_store(lv0 + 8 * (4 * q + 3), b); }
+    else { dg_load(in0 + 8 * (4 * q + 2), a); dg_load(in0 + 8 * (4 * q + 3), b); }
+    hnode(a, b, n1);
+    dg_store(lv1 + 8 * (2 * q + 1), n1);
+    hnode(n0, n1, out);
+}
+
+// Levels l+3, l+4 through LDS: 256 level-(l+2) nodes -> 128 -> 64.
+__device__ __forceinline__ void lds_two_levels(uint4* lds, const Dg& mine, uint32_t* lv2, uint32_t* lv3, uint32_t* lv4,
+                                               size_t g2 /*first level-(l+2) index of this WG*/) {
+    uint4* A = lds;            // 256 digests
+    uint4* B = lds + 512;      // 128 digests
+    const uint32_t t = threadIdx.x;
+    dg_store(lv2 + 8 * (g2 + t), mine);
+    dg_lds_store(A + 2 * t, mine);
+    __syncthreads();
+    if (t < 128) {
+        Dg l, r, o;
+        dg_lds_load(A + 4 * t, l); dg_lds_load(A + 4 * t + 2, r);
+        hnode(l, r, o);
+        dg_lds_store(B + 2 * t, o);
+        dg_store(lv3 + 8 * (g2 / 2 + t), o);
+    }
+    __syncthreads();
+    if (t < 64) {
+        Dg l, r, o;
+        dg_lds_load(B + 4 * t, l); dg_lds_load(B + 4 * t + 2, r);
+        hnode(l, r, o);
+        dg_store(lv4 + 8 * (g2 / 4 + t), o);
+    }
+}
+
+template <bool FOLD, bool COMMIT>
+__global__ __launch_bounds__(256) void k_layer_leaf(LayerTask t) {
+    if (COMMIT && FOLD && !t.st->active[t.k - 1]) return;
+    __shared__ uint4 lds[512 + 256];
+    __shared__ int32_t red[12];
+    const uint32_t L = t.L;
+    const size_t q = (size_t)blockIdx.x * 256 + threadIdx.x;   // quad index: leaves 4q..4q+3
+    uint4 v;
+    if (FOLD) {
+        const size_t half = (size_t)1 << L;
+        const uint32_t beta_m = COMMIT ? t.st->beta_mont[t.k - 1] : t.beta_m;
+        uint4 a = reinterpret_cast<const uint4*>(t.prev)[q];
+        uint4 b = reinterpret_cast<const uint4*>(t.prev + half)[q];
+        uint4 x = reinterpret_cast<const uint4*>(t.xinv)[q];
+        v.x = fold1(a.x, b.x, x.x, beta_m); v.y = fold1(a.y, b.y, x.y, beta_m);
+        v.z = fold1(a.z, b.z, x.z, beta_m); v.w = fold1(a.w, b.w, x.w, beta_m);
+        reinterpret_cast<uint4*>(t.values)[q] = v;
+    } else {
+        v = reinterpret_cast<const uint4*>(t.values)[q];
+    }
+    uint32_t* tr = t.tree;
+    Dg top;
+    quad<true>(v, nullptr, tr + 8 * level_offset(L, 0), tr + 8 * level_offset(L, 1), q, top);
+    if (COMMIT) coef_task(t, blockIdx.x, gridDim.x, red);
+    lds_two_levels(lds, top, tr + 8 * level_offset(L, 2), tr + 8 * level_offset(L, 3), tr + 8 * level_offset(L, 4),
+                   (size_t)blockIdx.x * 256);
+}
+
+// Mid tree: 1024 level-l nodes per workgroup -> 64 level-(l+4) nodes.
+__global__ __launch_bounds__(256) void k_tree_mid(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st, int gate) {
+    if (gate >= 0 && !st->active[gate]) return;
+    __shared__ uint4 lds[512 + 256];
+    const size_t q = (size_t)blockIdx.x * 256 + threadIdx.x;
+    Dg top;
+    uint4 dummy = make_uint4(0, 0, 0, 0);
+    quad<false>(dummy, tree + 8 * level_offset(L, l), nullptr, tree + 8 * level_offset(L, l + 1), q, top);
+    lds_two_levels(lds, top, tree + 8 * level_offset(L, l + 2), tree + 8 * level_offset(L, l + 3),
+                   tree + 8 * level_offset(L, l + 4), (size_t)blockIdx.x * 256);
+}
+
+// ------------------------------------------------------------ channel ----
+// Frozen spec: messages are built word by word in registers.
+__device__ __forceinline__ uint32_t hexch(uint32_t nib) { return nib < 10u ? 0x30u + nib : 0x57u + nib; }
+// 4 bytes -> 8 lowercase hex chars -> 2 big-endian message words
+__device__ __forceinline__ void hex2(uint32_t x, uint32_t& hi, uint32_t& lo) {
+    hi = (hexch(x >> 28) << 24) | (hexch((x >> 24) & 15u) << 16) | (hexch((x >> 20) & 15u) << 8) | hexch((x >> 16) & 15u);
+    lo = (hexch((x >> 12) & 15u) << 24) | (hexch((x >> 8) & 15u) << 16) | (hexch((x >> 4) & 15u) << 8) | hexch(x & 15u);
+}
+// one byte -> hex(hex(byte)) = 4 chars = one message word
+__device__ __forceinline__ uint32_t hexhex(uint32_t b) {
+    uint32_t c1 = hexch(b >> 4), c2 = hexch(b & 15u);
+    return (hexch(c1 >> 4) << 24) | (hexch(c1 & 15u) << 16) | (hexch(c2 >> 4) << 8) | hexch(c2 & 15u);
+}
+
+// channel.rs:35-44 with message = root_hex bytes: state = sha256_hex(state || hex(root_hex))
+__device__ void chan_send_root(DevState* st, const uint32_t root[8]) {
+    uint32_t s[8], w[16];
+    sha::init(s);
+    uint32_t len = 128;
+    if (st->chan_has) {
+        for (int i = 0; i < 8; i++) hex2(st->chan[i], w[2 * i], w[2 * i + 1]);
+        shaf::rounds_var(s, w);
+        len = 192;
+    }
+    for (int blk = 0; blk < 2; blk++) {
+        for (int j = 0; j < 16; j++) {
+            const int byte = blk * 16 + j;
+            w[j] = hexhex((root[byte >> 2] >> (24 - 8 * (byte & 3))) & 255u);
+        }
+        shaf::rounds_var(s, w);
+    }
+    for (int j = 0; j < 16; j++) w[j] = 0u;
+    w[0] = 0x80000000u;
+    w[15] = len * 8;
+    shaf::rounds_var(s, w);
+    for (int i = 0; i < 8; i++) st->chan[i] = s[i];
+    st->chan_has = 1;
+}
+
+// channel.rs:47-84: beta = U256(state) mod p; state = sha256_hex(state)
+__device__ uint32_t chan_receive_fe(DevState* st) {
+    uint64_t r = 0;
+    uint32_t w[16], s[8];
+    for (int i = 0; i < 8; i++) {
+        r = ((r << 32) | st->chan[i]) % P;
+        hex2(st->chan[i], w[2 * i], w[2 * i + 1]);
+    }
+    sha::init(s);
+    shaf::rounds_var(s, w);
+    shaf::rounds_pad64(s);
+    for (int i = 0; i < 8; i++) st->chan[i] = s[i];
+    return (uint32_t)r;
+}
+
+// fri_commit.rs:114: send(final.to_bytes()) — 8 bytes BE -> 16 hex chars
+__device__ void chan_send_final(DevState* st, uint32_t fv) {
+    uint32_t s[8], w[16];
+    sha::init(s);
+    uint32_t len = 16;
+    if (st->chan_has) {
+        for (int i = 0; i < 8; i++) hex2(st->chan[i], w[2 * i], w[2 * i + 1]);
+        shaf::rounds_var(s, w);
+        len = 80;
+    }
+    for (int j = 0; j < 16; j++) w[j] = 0u;
+    w[0] = 0x30303030u; w[1] = 0x30303030u;          // "00000000": high u32 of the u64 is 0
+    hex2(fv, w[2], w[3]);
+    w[4] = 0x80000000u;
+    w[15] = len * 8;
+    shaf::rounds_var(s, w);
+    for (int i = 0; i < 8; i++) st->chan[i] = s[i];
+    st->chan_has = 1;
+}
+
+// ---------------------------------------------------------------- top ----
+// One workgroup.  FROM_LEAVES: the layer has N = 2^L <= 1024 elements and is
+// done entirely here (fold, leaves, all levels, whole coefficient task).
+// Otherwise: N = 2^(L-l) <= 1024 level-l digests -> root.
+template <bool FROM_LEAVES, bool FOLD, bool COMMIT>
+__global__ __launch_bounds__(256) void k_tree_top(LayerTask t, uint32_t l, uint32_t G) {
+    if (COMMIT && t.k > 0 && !t.st->active[t.k - 1]) return;
+    __shared__ uint4 lds[2 * 1024 + 2 * 512];
+    __shared__ int32_t red[12];
+    const uint32_t L = t.L;
+    const uint32_t N = 1u << (L - l);
+    uint4* A = lds;
+    uint4* B = lds + 2 * 1024;
+    uint32_t* tr = t.tree;
+    if (FROM_LEAVES) {
+        const size_t half = (size_t)1 << L;
+        const uint32_t beta_m = FOLD ? (COMMIT ? t.st->beta_mont[t.k - 1] : t.beta_m) : 0u;
+        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+            uint32_t v;
+            if (FOLD) {
+                v = fold1(t.prev[i], t.prev[i + half], t.xinv[i], beta_m);
+                t.values[i] = v;
+            } else {
+                v = t.values[i];
+            }
+            Dg d;
+            hleaf(v, d);
+            dg_store(tr + 8 * i, d);
+            dg_lds_store(A + 2 * i, d);
+        }
+        if (COMMIT) coef_task(t, 0, 1, red);
+    } else {
+        const uint32_t* in = tr + 8 * level_offset(L, l);
+        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+            Dg d;
+            dg_load(in + 8 * i, d);
+            dg_lds_store(A + 2 * i, d);
+        }
+    }
+    __syncthreads();
+    uint32_t cnt = N;
+    for (uint32_t lv = l + 1; lv <= L; lv++) {
+        cnt >>= 1;
+        uint32_t* out = tr + 8 * level_offset(L, lv);
+#pragma unroll 1
+        for (uint32_t q = threadIdx.x; q < cnt; q += blockDim.x) {
+            Dg a, b, o;
+            dg_lds_load(A + 4 * q, a);
+            dg_lds_load(A + 4 * q + 2, b);
+            hnode(a, b, o);
+            dg_lds_store(B + 2 * q, o);
+            dg_store(out + 8 * q, o);
+        }
+        __syncthreads();
+        uint4* tmp = A; A = B; B = tmp;
+    }
+    if (!COMMIT) return;
+    // ---- degree of poly_k (reference degree field; see DevState) --------
+    DevState* st = t.st;
+    int m0 = -1, m1 = -1, m2 = -1;
+    for (uint32_t i = threadIdx.x; i < G; i += blockDim.x) {
+        m0 = max(m0, t.wgmax[3 * i]); m1 = max(m1, t.wgmax[3 * i + 1]); m2 = max(m2, t.wgmax[3 * i + 2]);
+    }
+    m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[3 * wave] = m0; red[3 * wave + 1] = m1; red[3 * wave + 2] = m2; }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int i = 1; i < 4; i++) { m0 = max(m0, red[3 * i]); m1 = max(m1, red[3 * i + 1]); m2 = max(m2, red[3 * i + 2]); }
+    const int k = t.k;
+    const int deg = (k == 0) ? m0 : (m1 < 0 ? m2 : m0);
+    st->deg[k] = deg;
+    Dg root;
+    dg_lds_load(A, root);
+    for (int i = 0; i < 8; i++) st->roots[k][i] = root.w[i];
+    chan_send_root(st, root.w);
+    st->n_layers = (uint32_t)k + 1;
+    if (deg >= 1 && k < MAXR && L >= 1) {
+        uint32_t beta = chan_receive_fe(st);
+        if (st->forced) beta = st->forced_beta[k];
+        st->beta[k] = beta;
+        st->beta_mont[k] = to_mont(beta);
+        st->active[k] = 1;
+        st->n_rounds = (uint32_t)k + 1;
+    } else {
+        st->active[k] = 0;
+        if (deg >= 1) { st->status = 7u; return; }            // FRI_EDEGREE
+        const uint32_t* ck = (k == 0) ? t.coef_in : t.coef_out;
+        uint32_t fv = (deg == -1) ? 0u : ck[0];
+        st->final_value = fv;
+        st->final_degree = deg;
+        chan_send_final(st, fv);
+    }
+}
+
+// ------------------------------------------------------------ launcher ----
+void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end) {
+    const uint32_t L = t.L;
+    const bool fold = t.prev != nullptr;
+    const bool commit = t.st != nullptr;
+    if (L <= TOP_LOG) {
+        if (fold) {
+            if (commit) hipLaunchKernelGGL((k_tree_top<true, true, true>), dim3(1), dim3(256), 0, s, t, 0u, 1u);
+            else hipLaunchKernelGGL((k_tree_top<true, true, false>), dim3(1), dim3(256), 0, s, t, 0u, 1u);
+        } else {
+            if (commit) hipLaunchKernelGGL((k_tree_top<true, false, true>), dim3(1), dim3(256), 0, s, t, 0u, 1u);
+            else hipLaunchKernelGGL((k_tree_top<true, false, false>), dim3(1), dim3(256), 0, s, t, 0u, 1u);
+        }
+        if (ev_leaf_end) hipEventRecord(ev_leaf_end, s);
+        return;
+    }
+    const uint32_t G = 1u << (L - 10);
+    if (fold) {
+        if (commit) hipLaunchKernelGGL((k_layer_leaf<true, true>), dim3(G), dim3(256), 0, s, t);
+        else hipLaunchKernelGGL((k_layer_leaf<true, false>), dim3(G), dim3(256), 0, s, t);
+    } else {
+        if (commit) hipLaunchKernelGGL((k_layer_leaf<false, true>), dim3(G), dim3(256), 0, s, t);
+        else hipLaunchKernelGGL((k_layer_leaf<false, false>), dim3(G), dim3(256), 0, s, t);
+    }
+    if (ev_leaf_end) hipEventRecord(ev_leaf_end, s);
+    const int gate = (commit && t.k > 0) ? t.k - 1 : -1;
+    uint32_t l = 4;
+    while (L - l > TOP_LOG) {
+        hipLaunchKernelGGL(k_tree_mid, dim3(1u << (L - l - 10)), dim3(256), 0, s, t.tree, L, l, t.st, gate);
+        l += 4;
+    }
+    if (commit) hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(256), 0, s, t, l, G);
+    else hipLaunchKernelGGL((k_tree_top<false, false, false>), dim3(1), dim3(256), 0, s, t, l, G);
+}
+
+}  // namespace fri

@@ -1,0 +1,125 @@
+// sha256_fast.hpp — gfx950 SHA-256 rounds written for the v_bitop3_b32 /
+// v_alignbit_b32 / v_add3_u32 instruction set (device only).
+//
+// Per round: Sigma1, Sigma0 = 3 alignbit + 1 bitop3(0x96 = xor3) each;
+// Ch = bitop3(0xCA); Maj = bitop3(0xE8); T1 = add3(h + K + W, Sigma1, Ch);
+// a' = add3(T1, Sigma0, Maj); e' = d + T1  ->  14 VALU ops.
+// Message schedule per word: sigma0/sigma1 = 2 alignbit + shift + bitop3,
+// w = add3(w16, s0, w7) + s1  ->  10 VALU ops.
+// The padding block of a 64-byte message (internal Merkle node) has a
+// constant schedule: K[t] + W[t] folds into one literal per round.
+#pragma once
+#include <stdint.h>
+#include "sha256.hpp"
+
+namespace fri {
+namespace shaf {
+
+// Constant operands (schedule words of the constant message parts) must
+// still fold at compile time, so the builtin is used only on live values.
+#define SHAF_CONST3(a, b, c) (__builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c))
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    if (SHAF_CONST3(a, b, c)) return a ^ b ^ c;
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t chf(uint32_t e, uint32_t f, uint32_t g) {
+    if (SHAF_CONST3(e, f, g)) return (e & f) ^ (~e & g);
+    return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);      // e ? f : g
+}
+__device__ __forceinline__ uint32_t majf(uint32_t a, uint32_t b, uint32_t c) {
+    if (SHAF_CONST3(a, b, c)) return (a & b) ^ (a & c) ^ (b & c);
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);      // majority
+}
+__device__ __forceinline__ uint32_t ror(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+__device__ __forceinline__ uint32_t S0(uint32_t a) { return xor3(ror(a, 2), ror(a, 13), ror(a, 22)); }
+__device__ __forceinline__ uint32_t S1(uint32_t e) { return xor3(ror(e, 6), ror(e, 11), ror(e, 25)); }
+__device__ __forceinline__ uint32_t s0(uint32_t x) { return xor3(ror(x, 7), ror(x, 18), x >> 3); }
+__device__ __forceinline__ uint32_t s1(uint32_t x) { return xor3(ror(x, 17), ror(x, 19), x >> 10); }
+
+// Host/compile-time schedule of the constant padding block of a 64-byte
+// message: W0 = 0x80000000, W15 = 512, others 0;  KWPAD[t] = K[t] + W[t].
+struct PadKW {
+    uint32_t kw[64];
+    constexpr PadKW() : kw() {
+        uint32_t w[64] = {};
+        w[0] = 0x80000000u;
+        w[15] = 512u;
+        for (int t = 16; t < 64; t++) {
+            uint32_t x = w[t - 15], y = w[t - 2];
+            uint32_t a = ((x >> 7) | (x << 25)) ^ ((x >> 18) | (x << 14)) ^ (x >> 3);
+            uint32_t b = ((y >> 17) | (y << 15)) ^ ((y >> 19) | (y << 13)) ^ (y >> 10);
+            w[t] = w[t - 16] + a + w[t - 7] + b;
+        }
+        constexpr uint32_t k[64] = {
+            0x428a2f98u,0x71374491u,0xb5c0fbcfu,0xe9b5dba5u,0x3956c25bu,0x59f111f1u,0x923f82a4u,0xab1c5ed5u,
+            0xd807aa98u,0x12835b01u,0x243185beu,0x550c7dc3u,0x72be5d74u,0x80deb1feu,0x9bdc06a7u,0xc19bf174u,
+            0xe49b69c1u,0xefbe4786u,0x0fc19dc6u,0x240ca1ccu,0x2de92c6fu,0x4a7484aau,0x5cb0a9dcu,0x76f988dau,
+            0x983e5152u,0xa831c66du,0xb00327c8u,0xbf597fc7u,0xc6e00bf3u,0xd5a79147u,0x06ca6351u,0x14292967u,
+            0x27b70a85u,0x2e1b2138u,0x4d2c6dfcu,0x53380d13u,0x650a7354u,0x766a0abbu,0x81c2c92eu,0x92722c85u,
+            0xa2bfe8a1u,0xa81a664bu,0xc24b8b70u,0xc76c51a3u,0xd192e819u,0xd6990624u,0xf40e3585u,0x106aa070u,
+            0x19a4c116u,0x1e376c08u,0x2748774cu,0x34b0bcb5u,0x391c0cb3u,0x4ed8aa4au,0x5b9cca4fu,0x682e6ff3u,
+            0x748f82eeu,0x78a5636fu,0x84c87814u,0x8cc70208u,0x90befffau,0xa4506cebu,0xbef9a3f7u,0xc67178f2u};
+        for (int t = 0; t < 64; t++) kw[t] = k[t] + w[t];
+    }
+};
+constexpr PadKW PAD_KW{};
+
+// Rounds on a register-resident schedule w[16] (consumed).  Variables are
+// rotated by renaming through the 8-way unrolled macro.
+__device__ __forceinline__ void rounds_var(uint32_t st[8], uint32_t w[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int t = 0; t < 64; t += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int tt = t + u;
+            uint32_t wt;
+            if (tt < 16) {
+                wt = w[tt];
+            } else {
+                wt = w[tt & 15] + s0(w[(tt - 15) & 15]) + w[(tt - 7) & 15] + s1(w[(tt - 2) & 15]);
+                w[tt & 15] = wt;
+            }
+            const uint32_t kw = sha::K(tt) + wt;
+            uint32_t t1 = h + kw + S1(e) + chf(e, f, g);
+            uint32_t t2 = S0(a) + majf(a, b, c);
+            h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Rounds on the constant padding block (64-byte message second block).
+__device__ __forceinline__ void rounds_pad64(uint32_t st[8]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int t = 0; t < 64; t++) {
+        uint32_t t1 = h + PAD_KW.kw[t] + S1(e) + chf(e, f, g);
+        uint32_t t2 = S0(a) + majf(a, b, c);
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Leaf: SHA256 of the 8-byte big-endian encoding of a u32 value.
+// Message words: W0 = 0, W1 = v, W2 = 0x80000000, W3..14 = 0, W15 = 64.
+// Round 0 (W0 = 0) is a compile-time constant after IV; the schedule words
+// that do not depend on v fold into literals.
+__device__ __forceinline__ void leaf(uint32_t v, uint32_t out[8]) {
+    uint32_t w[16] = {0u, v, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 64u};
+    sha::init(out);
+    rounds_var(out, w);
+}
+
+// Internal node: SHA256(l || r) = two compressions, second on the constant pad.
+__device__ __forceinline__ void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) { w[i] = l[i]; w[8 + i] = r[i]; }
+    sha::init(out);
+    rounds_var(out, w);
+    rounds_pad64(out);
+}
+
+}  // namespace shaf
+}  // namespace fri
