@@ -398,7 +398,7 @@ static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset) {
         hipMalloc(&p.trees, tre * 4) != hipSuccess || hipMalloc(&p.xinv, (xin ? xin : 1) * 4) != hipSuccess ||
         hipMalloc(&p.pre_lo, ((size_t)1 << POW_LO_LOG) * 4) != hipSuccess ||
         hipMalloc(&p.pre_hi, nhi * 4) != hipSuccess ||
-        hipMalloc(&p.wgmax, 3 * ((log_n > 10 ? ((size_t)1 << (log_n - 10)) : 1) + 1) * 4) != hipSuccess) {
+        hipMalloc(&p.wgmax, 6 * ((log_n > 10 ? ((size_t)1 << (log_n - 10)) : 1) + 16) * 4) != hipSuccess) {
         plan_free(ctx);
         return fail(ctx, FRI_ENOMEM, "device allocation failed for commit plan");
     }

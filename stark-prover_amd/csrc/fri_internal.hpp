@@ -9,9 +9,6 @@
 namespace fri {
 
 constexpr int MAXR = 32;            // == FRI_MAX_ROUNDS
-constexpr uint32_t NTT_TILE_LOG = 12;   // first-pass LDS tile: 4096 elements
-constexpr uint32_t NTT_MID_LOG = 10;    // middle-pass stages per launch
-constexpr uint32_t NTT_MID_W = 16;      // middle-pass contiguous run (64 B)
 constexpr uint32_t TOP_LOG = 10;        // single-workgroup tree top: <= 1024 inputs
 constexpr uint32_t POW_LO_LOG = 12;     // two-level power tables s^j = lo[j&4095]*hi[j>>12]
 

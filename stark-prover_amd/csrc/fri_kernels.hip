@@ -19,111 +19,183 @@
 namespace fri {
 
 // ============================================================== NTT ======
-// Natural order in -> natural order out.  Pass 1 gathers the input in
-// bit-reversed order (optionally scaled by pre(j) = s^j: the coset shift of
-// the LDE) into a 4096-element LDS tile and runs the first <= 12 DIT stages;
-// each further pass runs <= 10 stages on LDS tiles of 16 contiguous columns
-// x 1024 strided rows (64-byte coalesced runs).  Twiddles come from one
-// Montgomery table of the largest transform (index stride for smaller ones).
+// Natural order in -> natural order out, DIT after a bit-reversal gather.
+// Passes of NS <= 8 stages over 4096-element tiles (256 threads x 16
+// elements in registers): the first min(4, NS) stages run in registers on 16
+// consecutive tile elements, one LDS exchange, the remaining <= 4 stages run
+// in registers on stride-2^A groups, one LDS exchange back for coalesced
+// stores.  Pass 1 gathers input[bitrev(i)] (zero beyond d) scaled by pre(j)
+// = s^j (coset shift of the LDE); the last pass applies post(i) (n^-1 and
+// offset^-i for interpolation).  Later passes see the transform as columns
+// of 2^NS points at stride 2^s0; a workgroup takes 4096/2^NS consecutive
+// columns, so its loads/stores are contiguous runs across columns.
+// Twiddles: stage-packed table tw[2^s + j] = w_{2^(s+1)}^j (Montgomery).
 
 __device__ __forceinline__ uint32_t pow2lvl(const uint32_t* lo, const uint32_t* hi, size_t j, uint32_t v) {
     return mmul(mmul(v, hi[j >> POW_LO_LOG]), lo[j & ((1u << POW_LO_LOG) - 1)]);
 }
+__device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4); }
 
-__global__ __launch_bounds__(256) void k_ntt_first(const uint32_t* __restrict__ src, size_t d,
-                                                   uint32_t* __restrict__ dst, uint32_t log_n, uint32_t tb,
-                                                   const uint32_t* __restrict__ tw,
-                                                   const uint32_t* __restrict__ pre_lo,
-                                                   const uint32_t* __restrict__ pre_hi,
-                                                   const uint32_t* __restrict__ post_lo,
-                                                   const uint32_t* __restrict__ post_hi) {
-    __shared__ uint32_t lds[1u << NTT_TILE_LOG];
-    __shared__ uint32_t twl[1u << NTT_TILE_LOG];
-    const uint32_t T = 1u << tb;
-    const size_t base = (size_t)blockIdx.x << tb;
-    for (uint32_t i = threadIdx.x; i < T; i += blockDim.x) twl[i] = tw[i];
-    for (uint32_t i = threadIdx.x; i < T; i += blockDim.x) {
-        uint32_t pos = (uint32_t)(base + i);
-        uint32_t si = log_n ? (__brev(pos) >> (32 - log_n)) : 0u;
+template <int A, int B, bool FIRST>
+__global__ __launch_bounds__(256) void k_ntt_pass(const uint32_t* src, size_t d, uint32_t* dst,
+                                                  uint32_t log_n, uint32_t s0, const uint32_t* __restrict__ tw,
+                                                  const uint32_t* __restrict__ pre_lo, const uint32_t* __restrict__ pre_hi,
+                                                  const uint32_t* __restrict__ post_lo,
+                                                  const uint32_t* __restrict__ post_hi) {
+    constexpr uint32_t NS = A + B, P = 1u << NS, C = 4096u / P;
+    __shared__ uint32_t lds[4096 + 256];
+    const uint32_t tid = threadIdx.x;
+    const size_t ncols = ((size_t)1 << log_n) >> NS;
+    const size_t col0 = (size_t)blockIdx.x * C;
+    const size_t lomask = ((size_t)1 << s0) - 1;
+    auto gidx = [&](uint32_t c, uint32_t q) -> size_t {
+        const size_t col = col0 + c;
+        if (FIRST) return col * P + q;
+        return ((col >> s0) << (s0 + NS)) + ((size_t)q << s0) + (col & lomask);
+    };
+    // ---- load (contiguous runs) -------------------------------------------
+#pragma unroll 4
+    for (uint32_t r = 0; r < 16; r++) {
+        const uint32_t y = r * 256 + tid;
+        uint32_t c, q;
+        if (FIRST) { c = y / P; q = y % P; } else { c = y % C; q = y / C; }
         uint32_t v = 0;
-        if (si < d) {
-            v = src[si];
-            if (pre_lo) v = pow2lvl(pre_lo, pre_hi, si, v);
+        if (col0 + c < ncols) {
+            const size_t g = gidx(c, q);
+            if (FIRST) {
+                const uint32_t si = log_n ? (__brev((uint32_t)g) >> (32 - log_n)) : 0u;
+                if (si < d) {
+                    v = src[si];
+                    if (pre_lo) v = pow2lvl(pre_lo, pre_hi, si, v);
+                }
+            } else {
+                v = src[g];
+            }
         }
-        lds[i] = v;
+        lds[ntt_laddr(c * P + q)] = v;
     }
     __syncthreads();
-    for (uint32_t s = 0; s < tb; s++) {
-        const uint32_t h = 1u << s;
-        for (uint32_t b = threadIdx.x; b < T / 2; b += blockDim.x) {
-            uint32_t j = b & (h - 1);
-            uint32_t i0 = ((b >> s) << (s + 1)) + j, i1 = i0 + h;
-            uint32_t w = twl[h + j];
-            uint32_t u = lds[i0], v = mmul(lds[i1], w);
-            lds[i0] = add(u, v);
-            lds[i1] = sub(u, v);
+    uint32_t r[16];
+    // ---- phase A: stages 0..A-1 on 16 consecutive elements ----------------
+#pragma unroll
+    for (int e = 0; e < 16; e++) r[e] = lds[ntt_laddr(tid * 16 + e)];
+    {
+        const uint32_t x0 = tid * 16;
+        const uint32_t c = x0 >> NS;
+        const size_t lo = FIRST ? 0 : ((col0 + c) & lomask);
+#pragma unroll
+        for (int t = 0; t < A; t++) {
+            const uint32_t s = s0 + t;
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+                if (e & (1 << t)) continue;
+                const uint32_t q0 = (x0 + e) & (P - 1);
+                const size_t j = ((size_t)(q0 & ((1u << t) - 1)) << s0) + lo;
+                const uint32_t w = tw[((size_t)1 << s) + j];
+                const uint32_t u = r[e], v = mmul(r[e + (1 << t)], w);
+                r[e] = add(u, v);
+                r[e + (1 << t)] = sub(u, v);
+            }
+        }
+    }
+    if (B > 0) {
+#pragma unroll
+        for (int e = 0; e < 16; e++) lds[ntt_laddr(tid * 16 + e)] = r[e];
+        __syncthreads();
+        // ---- phase B: stages A..NS-1 on groups of 2^B at stride 2^A ---------
+        constexpr uint32_t GPT = 16u >> B;        // groups per thread
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            const uint32_t G = tid * GPT + (e >> B), m = e & ((1u << B) - 1);
+            const uint32_t c = G >> A, ql = G & ((1u << A) - 1);
+            r[e] = lds[ntt_laddr(c * P + ql + (m << A))];
+        }
+#pragma unroll
+        for (int t = A; t < (int)NS; t++) {
+            const uint32_t s = s0 + t, tb = t - A;
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+                if (e & (1 << tb)) continue;
+                const uint32_t G = tid * GPT + (e >> B), m = e & ((1u << B) - 1);
+                const uint32_t c = G >> A, ql = G & ((1u << A) - 1);
+                const uint32_t q0 = ql + (m << A);
+                const size_t lo = FIRST ? 0 : ((col0 + c) & lomask);
+                const size_t j = ((size_t)(q0 & ((1u << t) - 1)) << s0) + lo;
+                const uint32_t w = tw[((size_t)1 << s) + j];
+                const uint32_t u = r[e], v = mmul(r[e + (1 << tb)], w);
+                r[e] = add(u, v);
+                r[e + (1 << tb)] = sub(u, v);
+            }
         }
         __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            const uint32_t G = tid * GPT + (e >> B), m = e & ((1u << B) - 1);
+            const uint32_t c = G >> A, ql = G & ((1u << A) - 1);
+            lds[ntt_laddr(c * P + ql + (m << A))] = r[e];
+        }
+    } else {
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 16; e++) lds[ntt_laddr(tid * 16 + e)] = r[e];
     }
-    for (uint32_t i = threadIdx.x; i < T; i += blockDim.x) {
-        uint32_t v = lds[i];
-        if (post_lo) v = pow2lvl(post_lo, post_hi, base + i, v);
-        dst[base + i] = v;
+    __syncthreads();
+    // ---- store (contiguous runs) ------------------------------------------
+#pragma unroll 4
+    for (uint32_t rr = 0; rr < 16; rr++) {
+        const uint32_t y = rr * 256 + tid;
+        uint32_t c, q;
+        if (FIRST) { c = y / P; q = y % P; } else { c = y % C; q = y / C; }
+        if (col0 + c >= ncols) continue;
+        const size_t g = gidx(c, q);
+        uint32_t v = lds[ntt_laddr(c * P + q)];
+        if (post_lo) v = pow2lvl(post_lo, post_hi, g, v);
+        dst[g] = v;
     }
 }
 
-__global__ __launch_bounds__(256) void k_ntt_mid(uint32_t* __restrict__ data, uint32_t log_n, uint32_t s0,
-                                                 uint32_t ns, const uint32_t* __restrict__ tw,
-                                                 const uint32_t* __restrict__ post_lo,
-                                                 const uint32_t* __restrict__ post_hi) {
-    __shared__ uint32_t lds[NTT_MID_W << NTT_MID_LOG];
-    const uint32_t W = NTT_MID_W, M = 1u << ns;
-    const uint32_t nlo = (1u << s0) / W;
-    const uint32_t lo0 = (blockIdx.x % nlo) * W;
-    const size_t hib = ((size_t)(blockIdx.x / nlo)) << (s0 + ns);
-    for (uint32_t e = threadIdx.x; e < W * M; e += blockDim.x) {
-        uint32_t lo = e % W, mid = e / W;
-        lds[e] = data[hib + ((size_t)mid << s0) + lo0 + lo];
+__global__ void k_ntt_one(const uint32_t* src, size_t d, uint32_t* dst, const uint32_t* pre_lo,
+                          const uint32_t* pre_hi, const uint32_t* post_lo, const uint32_t* post_hi) {
+    if (threadIdx.x) return;
+    uint32_t v = d ? src[0] : 0u;
+    if (d && pre_lo) v = pow2lvl(pre_lo, pre_hi, 0, v);
+    if (post_lo) v = pow2lvl(post_lo, post_hi, 0, v);
+    dst[0] = v;
+}
+
+template <bool FIRST>
+static void launch_pass(uint32_t ns, const uint32_t* src, size_t d, uint32_t* dst, uint32_t log_n, uint32_t s0,
+                        const NttPlan& p, bool last, hipStream_t s) {
+    const size_t n = (size_t)1 << log_n;
+    const unsigned blocks = (unsigned)((n + 4095) / 4096);
+    const uint32_t* plo = FIRST ? p.pre_lo : nullptr;
+    const uint32_t* phi = FIRST ? p.pre_hi : nullptr;
+    const uint32_t* qlo = last ? p.post_lo : nullptr;
+    const uint32_t* qhi = last ? p.post_hi : nullptr;
+#define NTT_CASE(NSV, AV, BV)                                                                                   \
+    case NSV:                                                                                                   \
+        hipLaunchKernelGGL((k_ntt_pass<AV, BV, FIRST>), dim3(blocks), dim3(256), 0, s, src, d, dst, log_n, s0, p.tw, \
+                           plo, phi, qlo, qhi);                                                                 \
+        break;
+    switch (ns) {
+        NTT_CASE(1, 1, 0) NTT_CASE(2, 2, 0) NTT_CASE(3, 3, 0) NTT_CASE(4, 4, 0)
+        NTT_CASE(5, 4, 1) NTT_CASE(6, 4, 2) NTT_CASE(7, 4, 3) NTT_CASE(8, 4, 4)
+        default: break;
     }
-    __syncthreads();
-    for (uint32_t t = 0; t < ns; t++) {
-        const uint32_t s = s0 + t, hm = 1u << t;
-        for (uint32_t b = threadIdx.x; b < W * M / 2; b += blockDim.x) {
-            uint32_t lo = b % W, bm = b / W;
-            uint32_t jm = bm & (hm - 1);
-            uint32_t m0 = ((bm >> t) << (t + 1)) + jm, m1 = m0 + hm;
-            uint32_t j = lo0 + lo + (jm << s0);
-            uint32_t w = tw[((size_t)1 << s) + j];
-            uint32_t u = lds[m0 * W + lo], v = mmul(lds[m1 * W + lo], w);
-            lds[m0 * W + lo] = add(u, v);
-            lds[m1 * W + lo] = sub(u, v);
-        }
-        __syncthreads();
-    }
-    for (uint32_t e = threadIdx.x; e < W * M; e += blockDim.x) {
-        uint32_t lo = e % W, mid = e / W;
-        size_t idx = hib + ((size_t)mid << s0) + lo0 + lo;
-        uint32_t v = lds[e];
-        if (post_lo) v = pow2lvl(post_lo, post_hi, idx, v);
-        data[idx] = v;
-    }
+#undef NTT_CASE
 }
 
 void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, hipStream_t s) {
     const uint32_t log_n = p.log_n;
-    const uint32_t tb = log_n < NTT_TILE_LOG ? log_n : NTT_TILE_LOG;
-    const bool single = (tb == log_n);
-    const uint32_t nblk = 1u << (log_n - tb);
-    hipLaunchKernelGGL(k_ntt_first, dim3(nblk), dim3(256), 0, s, src, d, dst, log_n, tb, p.tw,
-                       p.pre_lo, p.pre_hi, single ? p.post_lo : nullptr, single ? p.post_hi : nullptr);
-    for (uint32_t s0 = tb; s0 < log_n;) {
-        uint32_t ns = (log_n - s0) < NTT_MID_LOG ? (log_n - s0) : NTT_MID_LOG;
-        bool last = (s0 + ns == log_n);
-        uint32_t blocks = (uint32_t)(((size_t)1 << log_n) / ((size_t)NTT_MID_W << ns));
-        hipLaunchKernelGGL(k_ntt_mid, dim3(blocks), dim3(256), 0, s, dst, log_n, s0, ns, p.tw,
-                           last ? p.post_lo : nullptr, last ? p.post_hi : nullptr);
-        s0 += ns;
+    if (log_n == 0) {   // one point: dst[0] = post(0) * pre(0) * src[0]
+        hipLaunchKernelGGL(k_ntt_one, dim3(1), dim3(64), 0, s, src, d, dst, p.pre_lo, p.pre_hi, p.post_lo, p.post_hi);
+        return;
     }
+    uint32_t first = log_n % 8;
+    if (first == 0) first = 8;
+    launch_pass<true>(first, src, d, dst, log_n, 0, p, first == log_n, s);
+    for (uint32_t s0 = first; s0 < log_n; s0 += 8)
+        launch_pass<false>(8, dst, 0, dst, log_n, s0, p, s0 + 8 == log_n, s);
 }
 
 // Stage-packed twiddles: tw[2^s + j] = Montgomery(w_{2^(s+1)}^j), so every

@@ -61,7 +61,7 @@ __device__ __forceinline__ int wave_max_i(int v) {
 // Coefficient task of one workgroup (w of G): k == 0 -> max nonzero index
 // of the input (deg_0); k >= 1 -> fold slice c'_j = c_2j + beta c_2j+1 with
 // maxima of c', even part, odd part.  Results: wgmax[3w .. 3w+2].
-__device__ void coef_task(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red /*LDS [3*4]*/) {
+__device__ void coef_task(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red /*LDS [3*waves]*/) {
     int m0 = -1, m1 = -1, m2 = -1;
     if (t.k == 0) {
         const size_t n = t.d0, cs = (n + G - 1) / G, lo = (size_t)w * cs, hi = min(n, lo + cs);
@@ -164,16 +164,50 @@ __global__ __launch_bounds__(256) void k_layer_leaf(LayerTask t) {
                    (size_t)blockIdx.x * 256);
 }
 
-// Mid tree: 1024 level-l nodes per workgroup -> 64 level-(l+4) nodes.
-__global__ __launch_bounds__(256) void k_tree_mid(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st, int gate) {
+// Reduce 16 coefficient-maxima triples (the 16 producer workgroups of this
+// workgroup's 1024 inputs) into one triple; lanes 0..15 of wave 0.
+__device__ __forceinline__ void reduce16(const int32_t* in, int32_t* out, uint32_t w, uint32_t nin) {
+    if (threadIdx.x >= 64) return;
+    const uint32_t i = 16 * w + threadIdx.x;
+    int a = -1, b = -1, c = -1;
+    if (threadIdx.x < 16 && i < nin) { a = in[3 * i]; b = in[3 * i + 1]; c = in[3 * i + 2]; }
+    a = wave_max_i(a); b = wave_max_i(b); c = wave_max_i(c);
+    if (threadIdx.x == 0) { out[3 * w] = a; out[3 * w + 1] = b; out[3 * w + 2] = c; }
+}
+
+// Mid tree (512 threads): 1024 level-l nodes per workgroup -> 64 level-(l+4)
+// nodes, one node per lane per level (latency-optimal on narrow levels).
+__global__ __launch_bounds__(512) void k_tree_mid(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st, int gate,
+                                                  const int32_t* mx_in, int32_t* mx_out, uint32_t nmx_in) {
     if (gate >= 0 && !st->active[gate]) return;
-    __shared__ uint4 lds[512 + 256];
-    const size_t q = (size_t)blockIdx.x * 256 + threadIdx.x;
-    Dg top;
-    uint4 dummy = make_uint4(0, 0, 0, 0);
-    quad<false>(dummy, tree + 8 * level_offset(L, l), nullptr, tree + 8 * level_offset(L, l + 1), q, top);
-    lds_two_levels(lds, top, tree + 8 * level_offset(L, l + 2), tree + 8 * level_offset(L, l + 3),
-                   tree + 8 * level_offset(L, l + 4), (size_t)blockIdx.x * 256);
+    __shared__ uint4 lds[2 * 1024 + 2 * 512];
+    uint4* A = lds;
+    uint4* B = lds + 2 * 1024;
+    const uint32_t t = threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * 1024;
+    const uint32_t* in = tree + 8 * level_offset(L, l);
+    Dg d0, d1;
+    dg_load(in + 8 * (base + t), d0);
+    dg_load(in + 8 * (base + t + 512), d1);
+    dg_lds_store(A + 2 * t, d0);
+    dg_lds_store(A + 2 * (t + 512), d1);
+    if (mx_in) reduce16(mx_in, mx_out, blockIdx.x, nmx_in);
+    __syncthreads();
+    uint32_t cnt = 1024;
+#pragma unroll 1
+    for (uint32_t j = 1; j <= 4; j++) {
+        cnt >>= 1;
+        if (t < cnt) {
+            Dg a, b, o;
+            dg_lds_load(A + 4 * t, a);
+            dg_lds_load(A + 4 * t + 2, b);
+            hnode(a, b, o);
+            dg_lds_store(B + 2 * t, o);
+            dg_store(tree + 8 * (level_offset(L, l + j) + (base >> j) + t), o);
+        }
+        __syncthreads();
+        uint4* tmp = A; A = B; B = tmp;
+    }
 }
 
 // ------------------------------------------------------------ channel ----
@@ -217,10 +251,12 @@ __device__ void chan_send_root(DevState* st, const uint32_t root[8]) {
 
 // channel.rs:47-84: beta = U256(state) mod p; state = sha256_hex(state)
 __device__ uint32_t chan_receive_fe(DevState* st) {
-    uint64_t r = 0;
+    uint32_t r = 0;
     uint32_t w[16], s[8];
     for (int i = 0; i < 8; i++) {
-        r = ((r << 32) | st->chan[i]) % P;
+        // r <- (r * 2^32 + w_i) mod p:  redc(r * R^2) = r * 2^32 mod p
+        const uint32_t wi = st->chan[i];
+        r = add(redc((uint64_t)r * R2_MOD_P), wi >= P ? wi - P : wi);
         hex2(st->chan[i], w[2 * i], w[2 * i + 1]);
     }
     sha::init(s);
@@ -255,10 +291,10 @@ __device__ void chan_send_final(DevState* st, uint32_t fv) {
 // done entirely here (fold, leaves, all levels, whole coefficient task).
 // Otherwise: N = 2^(L-l) <= 1024 level-l digests -> root.
 template <bool FROM_LEAVES, bool FOLD, bool COMMIT>
-__global__ __launch_bounds__(256) void k_tree_top(LayerTask t, uint32_t l, uint32_t G) {
+__global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const int32_t* mx, uint32_t G) {
     if (COMMIT && t.k > 0 && !t.st->active[t.k - 1]) return;
     __shared__ uint4 lds[2 * 1024 + 2 * 512];
-    __shared__ int32_t red[12];
+    __shared__ int32_t red[24];
     const uint32_t L = t.L;
     const uint32_t N = 1u << (L - l);
     uint4* A = lds;
@@ -280,7 +316,7 @@ __global__ __launch_bounds__(256) void k_tree_top(LayerTask t, uint32_t l, uint3
             dg_store(tr + 8 * i, d);
             dg_lds_store(A + 2 * i, d);
         }
-        if (COMMIT) coef_task(t, 0, 1, red);
+        if (COMMIT) { coef_task(t, 0, 1, red); mx = t.wgmax; G = 1; }
     } else {
         const uint32_t* in = tr + 8 * level_offset(L, l);
         for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
@@ -311,7 +347,7 @@ __global__ __launch_bounds__(256) void k_tree_top(LayerTask t, uint32_t l, uint3
     DevState* st = t.st;
     int m0 = -1, m1 = -1, m2 = -1;
     for (uint32_t i = threadIdx.x; i < G; i += blockDim.x) {
-        m0 = max(m0, t.wgmax[3 * i]); m1 = max(m1, t.wgmax[3 * i + 1]); m2 = max(m2, t.wgmax[3 * i + 2]);
+        m0 = max(m0, mx[3 * i]); m1 = max(m1, mx[3 * i + 1]); m2 = max(m2, mx[3 * i + 2]);
     }
     m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
     __syncthreads();
@@ -319,7 +355,7 @@ __global__ __launch_bounds__(256) void k_tree_top(LayerTask t, uint32_t l, uint3
     if ((threadIdx.x & 63) == 0) { red[3 * wave] = m0; red[3 * wave + 1] = m1; red[3 * wave + 2] = m2; }
     __syncthreads();
     if (threadIdx.x != 0) return;
-    for (int i = 1; i < 4; i++) { m0 = max(m0, red[3 * i]); m1 = max(m1, red[3 * i + 1]); m2 = max(m2, red[3 * i + 2]); }
+    for (uint32_t i = 1; i < blockDim.x / 64; i++) { m0 = max(m0, red[3 * i]); m1 = max(m1, red[3 * i + 1]); m2 = max(m2, red[3 * i + 2]); }
     const int k = t.k;
     const int deg = (k == 0) ? m0 : (m1 < 0 ? m2 : m0);
     st->deg[k] = deg;
@@ -353,16 +389,16 @@ void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end) {
     const bool commit = t.st != nullptr;
     if (L <= TOP_LOG) {
         if (fold) {
-            if (commit) hipLaunchKernelGGL((k_tree_top<true, true, true>), dim3(1), dim3(256), 0, s, t, 0u, 1u);
-            else hipLaunchKernelGGL((k_tree_top<true, true, false>), dim3(1), dim3(256), 0, s, t, 0u, 1u);
+            if (commit) hipLaunchKernelGGL((k_tree_top<true, true, true>), dim3(1), dim3(512), 0, s, t, 0u, (const int32_t*)nullptr, 1u);
+            else hipLaunchKernelGGL((k_tree_top<true, true, false>), dim3(1), dim3(512), 0, s, t, 0u, (const int32_t*)nullptr, 1u);
         } else {
-            if (commit) hipLaunchKernelGGL((k_tree_top<true, false, true>), dim3(1), dim3(256), 0, s, t, 0u, 1u);
-            else hipLaunchKernelGGL((k_tree_top<true, false, false>), dim3(1), dim3(256), 0, s, t, 0u, 1u);
+            if (commit) hipLaunchKernelGGL((k_tree_top<true, false, true>), dim3(1), dim3(512), 0, s, t, 0u, (const int32_t*)nullptr, 1u);
+            else hipLaunchKernelGGL((k_tree_top<true, false, false>), dim3(1), dim3(512), 0, s, t, 0u, (const int32_t*)nullptr, 1u);
         }
         if (ev_leaf_end) hipEventRecord(ev_leaf_end, s);
         return;
     }
-    const uint32_t G = 1u << (L - 10);
+    uint32_t G = 1u << (L - 10);
     if (fold) {
         if (commit) hipLaunchKernelGGL((k_layer_leaf<true, true>), dim3(G), dim3(256), 0, s, t);
         else hipLaunchKernelGGL((k_layer_leaf<true, false>), dim3(G), dim3(256), 0, s, t);
@@ -372,13 +408,21 @@ void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end) {
     }
     if (ev_leaf_end) hipEventRecord(ev_leaf_end, s);
     const int gate = (commit && t.k > 0) ? t.k - 1 : -1;
+    // coefficient maxima: level 0 at wgmax[0 .. 3G), each mid kernel reduces 16:1
+    int32_t* mx = t.wgmax;
+    size_t mx_off = 3 * (size_t)G;
     uint32_t l = 4;
     while (L - l > TOP_LOG) {
-        hipLaunchKernelGGL(k_tree_mid, dim3(1u << (L - l - 10)), dim3(256), 0, s, t.tree, L, l, t.st, gate);
+        const uint32_t grid = 1u << (L - l - 10);
+        int32_t* mx_out = commit ? t.wgmax + mx_off : nullptr;
+        hipLaunchKernelGGL(k_tree_mid, dim3(grid), dim3(512), 0, s, t.tree, L, l, t.st, gate,
+                           commit ? (const int32_t*)mx : (const int32_t*)nullptr, mx_out, G);
+        if (commit) { mx = mx_out; mx_off += 3 * (size_t)grid; }
+        G = grid;
         l += 4;
     }
-    if (commit) hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(256), 0, s, t, l, G);
-    else hipLaunchKernelGGL((k_tree_top<false, false, false>), dim3(1), dim3(256), 0, s, t, l, G);
+    if (commit) hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, (const int32_t*)mx, G);
+    else hipLaunchKernelGGL((k_tree_top<false, false, false>), dim3(1), dim3(512), 0, s, t, l, (const int32_t*)nullptr, G);
 }
 
 }  // namespace fri
