@@ -168,6 +168,10 @@ int fri_set_profiling(fri_ctx* ctx, int enabled);
 int fri_get_profile(fri_ctx* ctx, const char* kernel_class, double* total_ms, uint64_t* launches,
                     uint64_t* bytes);
 int fri_reset_profile(fri_ctx* ctx);
+/* Diagnostic build only (-DFRI_STAMPS): top-kernel phase timestamps of the
+ * last commit, (FRI_MAX_LAYERS x 24) u64 ticks of the 100 MHz clock.
+ * Returns FRI_ESTATE in the product build. */
+int fri_debug_stamps(fri_ctx* ctx, uint64_t* out, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,11 @@ using namespace fri;
 
 template <int V>
 __device__ __forceinline__ void do_node(const uint32_t* l, const uint32_t* r, uint32_t* o) {
-    if (V == 1) sha::node(l, r, o); else shaf::node(l, r, o);
+    if (V == 1) sha::node(l, r, o); else if (V == 2) shaf::node(l, r, o); else if (V == 3) shaf::node_compact(l, r, o);
+    else if (V == 4) { uint32_t w[16]; for (int i = 0; i < 8; i++) { w[i] = l[i]; w[8 + i] = r[i]; } sha::init(o); shaf::compress_loop(o, w); }
+    else if (V == 5) { for (int i = 0; i < 8; i++) o[i] = l[i]; shaf::kwtab_loop(o, shaf::PAD_KW_C.kw); }
+    else if (V == 6) { for (int i = 0; i < 8; i++) o[i] = l[i]; shaf::rounds_pad64(o); }
+    else if (V == 7) { uint32_t w[16]; for (int i = 0; i < 8; i++) { w[i] = l[i]; w[8 + i] = r[i]; } sha::init(o); shaf::rounds_var(o, w); }
 }
 template <int V>
 __device__ __forceinline__ void do_leaf(uint32_t v, uint32_t* o) {
@@ -169,11 +173,22 @@ int main() {
     rep("node v2 lb1 grid2048", timeit([&] { hipLaunchKernelGGL((k_node<2, 1>), dim3(2048), dim3(256), 0, 0, nin, out, n); }, it), 2.0 * n, 1450);
     {
         uint32_t* o; CK(hipMalloc(&o, 64 * 8 * 4));
-        for (int v = 1; v <= 2; v++) {
+        const char* nm[8] = {"", "node v1 (plain C)", "node v2 (bitop3, unrolled)", "node compact (looped)",
+                             "compress_loop (var block)", "kwtab_loop (pad block)", "rounds_pad64 (unrolled)",
+                             "rounds_var (unrolled var)"};
+        for (int v = 1; v <= 7; v++) {
             int nch = 256;
-            float ms = timeit([&] { if (v == 1) hipLaunchKernelGGL((k_chain<1>), dim3(1), dim3(64), 0, 0, o, nch);
-                                    else hipLaunchKernelGGL((k_chain<2>), dim3(1), dim3(64), 0, 0, o, nch); }, 3);
-            printf("single-wave node-hash latency v%d: %.2f us per node\n", v, ms * 1e3 / nch);
+            float ms = timeit([&] {
+                switch (v) {
+                    case 1: hipLaunchKernelGGL((k_chain<1>), dim3(1), dim3(64), 0, 0, o, nch); break;
+                    case 2: hipLaunchKernelGGL((k_chain<2>), dim3(1), dim3(64), 0, 0, o, nch); break;
+                    case 3: hipLaunchKernelGGL((k_chain<3>), dim3(1), dim3(64), 0, 0, o, nch); break;
+                    case 4: hipLaunchKernelGGL((k_chain<4>), dim3(1), dim3(64), 0, 0, o, nch); break;
+                    case 5: hipLaunchKernelGGL((k_chain<5>), dim3(1), dim3(64), 0, 0, o, nch); break;
+                    case 6: hipLaunchKernelGGL((k_chain<6>), dim3(1), dim3(64), 0, 0, o, nch); break;
+                    case 7: hipLaunchKernelGGL((k_chain<7>), dim3(1), dim3(64), 0, 0, o, nch); break;
+                } }, 3);
+            printf("single-wave latency %-28s %.2f us\n", nm[v], ms * 1e3 / nch);
         }
     }
     {

@@ -1,0 +1,25 @@
+"""Diagnostic: per-layer top-kernel phase durations (us) from the FRI_STAMPS
+build.  Usage: FRI_AMD_LIB=libfri_amd_stamps.so python stark-prover_amd/bench/stamps.py"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "python"))
+import fri_amd  # noqa: E402
+
+log_n = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+d = 1 << (log_n - 3)
+ctx = fri_amd.Context(0, log_n)
+c = (np.arange(d, dtype=np.uint64) * 2654435761 % fri_amd.P).astype(np.uint32)
+for _ in range(3):
+    res = ctx.commit(c, log_n)
+buf = (ctypes.c_uint64 * (33 * 24))()
+ctx._check(ctx.lib.fri_debug_stamps(ctx.h, buf, 33 * 24))
+a = np.frombuffer(buf, dtype=np.uint64).reshape(33, 24).astype(np.int64)
+for k in range(res.n_layers):
+    row = a[k]
+    t0 = row[0]
+    marks = [(i, (row[i] - t0) / 100.0) for i in range(1, 24) if row[i] > 0]
+    print(f"layer {k:2d} L={log_n - k:2d}: " + " ".join(f"{i}:{us:.1f}" for i, us in marks))

@@ -398,7 +398,7 @@ static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset) {
         hipMalloc(&p.trees, tre * 4) != hipSuccess || hipMalloc(&p.xinv, (xin ? xin : 1) * 4) != hipSuccess ||
         hipMalloc(&p.pre_lo, ((size_t)1 << POW_LO_LOG) * 4) != hipSuccess ||
         hipMalloc(&p.pre_hi, nhi * 4) != hipSuccess ||
-        hipMalloc(&p.wgmax, 6 * ((log_n > 10 ? ((size_t)1 << (log_n - 10)) : 1) + 16) * 4) != hipSuccess) {
+        hipMalloc(&p.wgmax, 6 * ((log_n > 8 ? ((size_t)1 << (log_n - 8)) : 1) + 16) * 4) != hipSuccess) {
         plan_free(ctx);
         return fail(ctx, FRI_ENOMEM, "device allocation failed for commit plan");
     }
@@ -461,7 +461,7 @@ static void enqueue_commit(fri_ctx* ctx) {
         uint64_t leaf_nodes = 0;
         for (uint32_t j = 0; j <= 4 && j <= L; j++) leaf_nodes += (uint64_t)1 << (L - j);
         const uint64_t leaf_bytes = ((uint64_t)4 << L) + 4 * (uint64_t)p.d + 32 * leaf_nodes;
-        size_t spl = (k == 0 && L > TOP_LOG) ? span_begin(ctx, "merkle_layer0_leaf", leaf_bytes) : (size_t)-1;
+        size_t spl = (k == 0 && L >= 19) ? span_begin(ctx, "merkle_layer0_leaf", leaf_bytes) : (size_t)-1;
         size_t spk = span_begin(ctx, k == 0 ? "layer0" : "layers", 0);
         launch_layer(t, s, spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
         span_end(ctx, spk);
@@ -611,6 +611,21 @@ extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint3
     }
     *depth_out = L;
     return FRI_OK;
+}
+
+// Diagnostic: per-layer top-kernel phase stamps of the last commit
+// (100 MHz ticks), only in the -DFRI_STAMPS build.
+extern "C" int fri_debug_stamps(fri_ctx* ctx, uint64_t* out, size_t cap) {
+    if (!ctx || !out) return FRI_EINVAL;
+#ifdef FRI_STAMPS
+    const size_t n = sizeof(ctx->h_state->stamps) / sizeof(uint64_t);
+    if (cap < n) return fail(ctx, FRI_EINVAL, "buffer too small");
+    memcpy(out, ctx->h_state->stamps, sizeof(ctx->h_state->stamps));
+    return FRI_OK;
+#else
+    (void)cap;
+    return fail(ctx, FRI_ESTATE, "library built without FRI_STAMPS");
+#endif
 }
 
 extern "C" int fri_set_profiling(fri_ctx* ctx, int enabled) {

@@ -9,7 +9,7 @@
 namespace fri {
 
 constexpr int MAXR = 32;            // == FRI_MAX_ROUNDS
-constexpr uint32_t TOP_LOG = 10;        // single-workgroup tree top: <= 1024 inputs
+constexpr uint32_t TOP_LOG = 9;         // single-workgroup tree top: <= 512 inputs
 constexpr uint32_t POW_LO_LOG = 12;     // two-level power tables s^j = lo[j&4095]*hi[j>>12]
 
 // Device-resident commit state (one per context).  Every per-round kernel
@@ -19,6 +19,7 @@ constexpr uint32_t POW_LO_LOG = 12;     // two-level power tables s^j = lo[j&409
 struct DevState {
     uint32_t chan[8];            // channel state digest (src/channel/channel.rs:19)
     uint32_t chan_has;           // 0 => state == ""
+    uint32_t chan_pending;       // 1 => true state = sha256_hex(hex(chan)) (receive's rehash deferred)
     uint32_t n_layers;
     uint32_t n_rounds;
     uint32_t final_value;
@@ -35,6 +36,9 @@ struct DevState {
     uint32_t beta_mont[MAXR];
     uint32_t forced_beta[MAXR];
     uint32_t roots[MAXR + 1][8];
+#ifdef FRI_STAMPS
+    uint64_t stamps[MAXR + 1][24];   // diagnostic build only: s_memrealtime (100 MHz) per phase
+#endif
 };
 
 // Tree layout: layer with 2^L leaves stores levels 0..L contiguously,

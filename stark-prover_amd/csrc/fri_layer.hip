@@ -26,6 +26,17 @@ namespace fri {
 
 constexpr uint32_t INV2_M2 = 0x80000000u;   // Montgomery(2^-1) = 2^31 mod p
 
+// Diagnostic build (-DFRI_STAMPS, lib/libfri_amd_stamps.so): thread 0 of a
+// top kernel records s_memrealtime at phase boundaries.  Never in the product.
+#ifdef FRI_STAMPS
+#define TOP_STAMP(i)                                                                     \
+    do {                                                                                 \
+        if (COMMIT && threadIdx.x == 0) t.st->stamps[t.k][(i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define TOP_STAMP(i) do {} while (0)
+#endif
+
 __device__ __forceinline__ uint32_t fold1(uint32_t a, uint32_t b, uint32_t xinv_m, uint32_t beta_m) {
     uint32_t s = add(a, b), t = sub(a, b);
     return mmul(add(s, mmul(mmul(t, xinv_m), beta_m)), INV2_M2);
@@ -51,6 +62,16 @@ __device__ __forceinline__ void dg_lds_store(uint4* p, const Dg& d) {
 }
 __device__ __forceinline__ void hnode(const Dg& l, const Dg& r, Dg& o) { shaf::node(l.w, r.w, o.w); }
 __device__ __forceinline__ void hleaf(uint32_t v, Dg& o) { shaf::leaf(v, o.w); }
+// compact (looped) forms for the latency-bound mid / top kernels
+__device__ __forceinline__ void cnode(const Dg& l, const Dg& r, Dg& o) { shaf::node_compact(l.w, r.w, o.w); }
+__device__ __forceinline__ void cleaf(uint32_t v, Dg& o) { shaf::leaf_compact(v, o.w); }
+
+// Barrier that waits only for this wave's LDS traffic: HIP's __syncthreads()
+// also drains vmcnt, i.e. waits ~1 us for the level's global digest stores,
+// which no other wave of the workgroup reads.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
@@ -61,7 +82,7 @@ __device__ __forceinline__ int wave_max_i(int v) {
 // Coefficient task of one workgroup (w of G): k == 0 -> max nonzero index
 // of the input (deg_0); k >= 1 -> fold slice c'_j = c_2j + beta c_2j+1 with
 // maxima of c', even part, odd part.  Results: wgmax[3w .. 3w+2].
-__device__ void coef_task(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red /*LDS [3*waves]*/) {
+__device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red /*LDS [3*waves]*/) {
     int m0 = -1, m1 = -1, m2 = -1;
     if (t.k == 0) {
         const size_t n = t.d0, cs = (n + G - 1) / G, lo = (size_t)w * cs, hi = min(n, lo + cs);
@@ -119,7 +140,7 @@ __device__ __forceinline__ void lds_two_levels(uint4* lds, const Dg& mine, uint3
     const uint32_t t = threadIdx.x;
     dg_store(lv2 + 8 * (g2 + t), mine);
     dg_lds_store(A + 2 * t, mine);
-    __syncthreads();
+    lds_barrier();
     if (t < 128) {
         Dg l, r, o;
         dg_lds_load(A + 4 * t, l); dg_lds_load(A + 4 * t + 2, r);
@@ -127,7 +148,7 @@ __device__ __forceinline__ void lds_two_levels(uint4* lds, const Dg& mine, uint3
         dg_lds_store(B + 2 * t, o);
         dg_store(lv3 + 8 * (g2 / 2 + t), o);
     }
-    __syncthreads();
+    lds_barrier();
     if (t < 64) {
         Dg l, r, o;
         dg_lds_load(B + 4 * t, l); dg_lds_load(B + 4 * t + 2, r);
@@ -164,36 +185,83 @@ __global__ __launch_bounds__(256) void k_layer_leaf(LayerTask t) {
                    (size_t)blockIdx.x * 256);
 }
 
-// Reduce 16 coefficient-maxima triples (the 16 producer workgroups of this
-// workgroup's 1024 inputs) into one triple; lanes 0..15 of wave 0.
-__device__ __forceinline__ void reduce16(const int32_t* in, int32_t* out, uint32_t w, uint32_t nin) {
+// Wide leaf kernel for narrow layers (2^10 .. 2^18 elements): one leaf per
+// lane, 256 leaves per workgroup, levels 1..4 through LDS (one node per lane
+// per level): latency 1 leaf + 4 nodes instead of the quad form's 4 + 5.
+template <bool FOLD, bool COMMIT>
+__global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
+    if (COMMIT && FOLD && !t.st->active[t.k - 1]) return;
+    __shared__ uint4 lds[2 * 256 + 2 * 128];
+    __shared__ int32_t red[12];
+    const uint32_t L = t.L;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t v;
+    if (FOLD) {
+        const size_t half = (size_t)1 << L;
+        const uint32_t beta_m = COMMIT ? t.st->beta_mont[t.k - 1] : t.beta_m;
+        v = fold1(t.prev[i], t.prev[i + half], t.xinv[i], beta_m);
+        t.values[i] = v;
+    } else {
+        v = t.values[i];
+    }
+    uint32_t* tr = t.tree;
+    Dg d;
+    hleaf(v, d);
+    dg_store(tr + 8 * i, d);
+    uint4* A = lds;
+    uint4* B = lds + 2 * 256;
+    dg_lds_store(A + 2 * threadIdx.x, d);
+    if (COMMIT) coef_task(t, blockIdx.x, gridDim.x, red);
+    lds_barrier();
+    uint32_t cnt = 256;
+#pragma unroll 1
+    for (uint32_t j = 1; j <= 4; j++) {
+        cnt >>= 1;
+        if (threadIdx.x < cnt) {
+            Dg a, b, o;
+            dg_lds_load(A + 4 * threadIdx.x, a);
+            dg_lds_load(A + 4 * threadIdx.x + 2, b);
+            hnode(a, b, o);
+            dg_lds_store(B + 2 * threadIdx.x, o);
+            dg_store(tr + 8 * (level_offset(L, j) + ((size_t)blockIdx.x << (8 - j)) + threadIdx.x), o);
+        }
+        lds_barrier();
+        uint4* tmp = A; A = B; B = tmp;
+    }
+}
+
+// Reduce the coefficient-maxima triples of the R producer workgroups of this
+// workgroup's inputs (R <= 64) into one triple (wave 0).
+__device__ __forceinline__ void reduce_mx(const int32_t* in, int32_t* out, uint32_t w, uint32_t R) {
     if (threadIdx.x >= 64) return;
-    const uint32_t i = 16 * w + threadIdx.x;
+    const uint32_t i = R * w + threadIdx.x;
     int a = -1, b = -1, c = -1;
-    if (threadIdx.x < 16 && i < nin) { a = in[3 * i]; b = in[3 * i + 1]; c = in[3 * i + 2]; }
+    if (threadIdx.x < R) { a = in[3 * i]; b = in[3 * i + 1]; c = in[3 * i + 2]; }
     a = wave_max_i(a); b = wave_max_i(b); c = wave_max_i(c);
     if (threadIdx.x == 0) { out[3 * w] = a; out[3 * w + 1] = b; out[3 * w + 2] = c; }
 }
 
-// Mid tree (512 threads): 1024 level-l nodes per workgroup -> 64 level-(l+4)
-// nodes, one node per lane per level (latency-optimal on narrow levels).
-__global__ __launch_bounds__(512) void k_tree_mid(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st, int gate,
-                                                  const int32_t* mx_in, int32_t* mx_out, uint32_t nmx_in) {
+// Mid tree: NIN level-l nodes per workgroup -> NIN/16 level-(l+4) nodes,
+// one node per lane per level.  NIN = 1024 (512 threads) for wide levels,
+// 256 (128 threads: one wave per SIMD on every level) for narrow ones.
+template <uint32_t NIN>
+__global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st,
+                                                      int gate, const int32_t* mx_in, int32_t* mx_out, uint32_t R) {
     if (gate >= 0 && !st->active[gate]) return;
-    __shared__ uint4 lds[2 * 1024 + 2 * 512];
+    __shared__ uint4 lds[2 * NIN + NIN];
     uint4* A = lds;
-    uint4* B = lds + 2 * 1024;
+    uint4* B = lds + 2 * NIN;
     const uint32_t t = threadIdx.x;
-    const size_t base = (size_t)blockIdx.x * 1024;
+    const size_t base = (size_t)blockIdx.x * NIN;
     const uint32_t* in = tree + 8 * level_offset(L, l);
     Dg d0, d1;
     dg_load(in + 8 * (base + t), d0);
-    dg_load(in + 8 * (base + t + 512), d1);
+    dg_load(in + 8 * (base + t + NIN / 2), d1);
     dg_lds_store(A + 2 * t, d0);
-    dg_lds_store(A + 2 * (t + 512), d1);
-    if (mx_in) reduce16(mx_in, mx_out, blockIdx.x, nmx_in);
-    __syncthreads();
-    uint32_t cnt = 1024;
+    dg_lds_store(A + 2 * (t + NIN / 2), d1);
+    if (mx_in) reduce_mx(mx_in, mx_out, blockIdx.x, R);
+    lds_barrier();
+    uint32_t cnt = NIN;
 #pragma unroll 1
     for (uint32_t j = 1; j <= 4; j++) {
         cnt >>= 1;
@@ -205,7 +273,7 @@ __global__ __launch_bounds__(512) void k_tree_mid(uint32_t* tree, uint32_t L, ui
             dg_lds_store(B + 2 * t, o);
             dg_store(tree + 8 * (level_offset(L, l + j) + (base >> j) + t), o);
         }
-        __syncthreads();
+        lds_barrier();
         uint4* tmp = A; A = B; B = tmp;
     }
 }
@@ -218,72 +286,99 @@ __device__ __forceinline__ void hex2(uint32_t x, uint32_t& hi, uint32_t& lo) {
     hi = (hexch(x >> 28) << 24) | (hexch((x >> 24) & 15u) << 16) | (hexch((x >> 20) & 15u) << 8) | hexch((x >> 16) & 15u);
     lo = (hexch((x >> 12) & 15u) << 24) | (hexch((x >> 8) & 15u) << 16) | (hexch((x >> 4) & 15u) << 8) | hexch(x & 15u);
 }
-// one byte -> hex(hex(byte)) = 4 chars = one message word
+// one byte -> hex(hex(byte)) = 4 chars = one message word.  For a nibble n,
+// hexch(n) is '0'+n or 'a'+n-10, whose own hex is "3" '0'+n or "6" '0'+n-9:
+// 0x3330 + n, plus 0x2F7 when n >= 10 (two 16-bit SWAR lanes).
 __device__ __forceinline__ uint32_t hexhex(uint32_t b) {
-    uint32_t c1 = hexch(b >> 4), c2 = hexch(b & 15u);
-    return (hexch(c1 >> 4) << 24) | (hexch(c1 & 15u) << 16) | (hexch(c2 >> 4) << 8) | hexch(c2 & 15u);
+    const uint32_t x = ((b & 0xF0u) << 12) | (b & 0x0Fu);
+    const uint32_t ge = ((x + 0x00060006u) >> 4) & 0x00010001u;
+    return 0x33303330u + x + ge * 0x2F7u;
 }
 
-// channel.rs:35-44 with message = root_hex bytes: state = sha256_hex(state || hex(root_hex))
-__device__ void chan_send_root(DevState* st, const uint32_t root[8]) {
-    uint32_t s[8], w[16];
-    sha::init(s);
-    uint32_t len = 128;
-    if (st->chan_has) {
-        for (int i = 0; i < 8; i++) hex2(st->chan[i], w[2 * i], w[2 * i + 1]);
-        shaf::rounds_var(s, w);
-        len = 192;
+// Channel prework (off the critical path, done by an idle wave during the
+// narrow tree levels): the deferred rehash of the previous receive
+// (channel.rs:75-76, state = sha256_hex(state)) and the midstate of the next
+// send's first block hex(state) (channel.rs:36-39).  Three steps, one
+// compression each; steps that do not apply are skipped.
+struct ChanPre {
+    uint32_t st[8];      // true current state (after the deferred rehash)
+    uint32_t mid[8];     // compress(IV, hex(st))
+    int step;            // next step: 0 rehash block, 1 rehash pad, 2 midstate, 3 done
+};
+__device__ __forceinline__ void chanpre_init(ChanPre& c, const DevState* st) {
+    #pragma unroll
+    for (int i = 0; i < 8; i++) c.st[i] = st->chan[i];
+    c.step = !st->chan_has ? 3 : (st->chan_pending ? 0 : 2);
+}
+__device__ __forceinline__ void chanpre_step(ChanPre& c) {  // compact forms: off the critical path
+    uint32_t w[16];
+    if (c.step == 0) {
+        #pragma unroll
+        for (int i = 0; i < 8; i++) hex2(c.st[i], w[2 * i], w[2 * i + 1]);
+        sha::init(c.mid);
+        shaf::compress_loop(c.mid, w);            // mid used as scratch for the rehash
+    } else if (c.step == 1) {
+        shaf::kwtab_loop(c.mid, shaf::PAD_KW_C.kw);
+        #pragma unroll
+        for (int i = 0; i < 8; i++) c.st[i] = c.mid[i];
+    } else if (c.step == 2) {
+        #pragma unroll
+        for (int i = 0; i < 8; i++) hex2(c.st[i], w[2 * i], w[2 * i + 1]);
+        sha::init(c.mid);
+        shaf::compress_loop(c.mid, w);
     }
+    c.step++;
+}
+
+// channel.rs:35-44 with message = root_hex bytes (frozen spec):
+// state = sha256_hex(state || hex(root_hex)).  `mid` = compress(IV, hex(state))
+// when has_state; the two hex(hex(root)) blocks and the constant padding
+// block remain (3 compressions).
+__device__ __forceinline__ void chan_send_root(uint32_t has, const uint32_t mid[8], const uint32_t root[8],
+                                               uint32_t out[8]) {
+    uint32_t w[16];
+    if (has) { for (int i = 0; i < 8; i++) out[i] = mid[i]; }
+    else sha::init(out);
+    #pragma unroll
     for (int blk = 0; blk < 2; blk++) {
+        #pragma unroll
         for (int j = 0; j < 16; j++) {
             const int byte = blk * 16 + j;
             w[j] = hexhex((root[byte >> 2] >> (24 - 8 * (byte & 3))) & 255u);
         }
-        shaf::rounds_var(s, w);
+        shaf::compress_loop(out, w);
     }
-    for (int j = 0; j < 16; j++) w[j] = 0u;
-    w[0] = 0x80000000u;
-    w[15] = len * 8;
-    shaf::rounds_var(s, w);
-    for (int i = 0; i < 8; i++) st->chan[i] = s[i];
-    st->chan_has = 1;
+    shaf::kwtab_loop(out, has ? shaf::PAD_KW_1536.kw : shaf::PAD_KW_1024.kw);
 }
 
-// channel.rs:47-84: beta = U256(state) mod p; state = sha256_hex(state)
-__device__ uint32_t chan_receive_fe(DevState* st) {
+// channel.rs:47-72: beta = U256(state) mod p  (the rehash is deferred)
+__device__ __forceinline__ uint32_t chan_beta(const uint32_t s[8]) {
     uint32_t r = 0;
-    uint32_t w[16], s[8];
+    #pragma unroll
     for (int i = 0; i < 8; i++) {
         // r <- (r * 2^32 + w_i) mod p:  redc(r * R^2) = r * 2^32 mod p
-        const uint32_t wi = st->chan[i];
+        const uint32_t wi = s[i];
         r = add(redc((uint64_t)r * R2_MOD_P), wi >= P ? wi - P : wi);
-        hex2(st->chan[i], w[2 * i], w[2 * i + 1]);
     }
-    sha::init(s);
-    shaf::rounds_var(s, w);
-    shaf::rounds_pad64(s);
-    for (int i = 0; i < 8; i++) st->chan[i] = s[i];
-    return (uint32_t)r;
+    return r;
 }
 
-// fri_commit.rs:114: send(final.to_bytes()) — 8 bytes BE -> 16 hex chars
-__device__ void chan_send_final(DevState* st, uint32_t fv) {
-    uint32_t s[8], w[16];
-    sha::init(s);
-    uint32_t len = 16;
-    if (st->chan_has) {
-        for (int i = 0; i < 8; i++) hex2(st->chan[i], w[2 * i], w[2 * i + 1]);
-        shaf::rounds_var(s, w);
-        len = 80;
-    }
+// fri_commit.rs:114: send(final.to_bytes()) — state || 16 hex chars of the
+// 8-byte big-endian value.  `s` is the state right after the last root send
+// (no receive in between, so no rehash).
+__device__ __forceinline__ void chan_send_final(const uint32_t s[8], uint32_t fv, uint32_t out[8]) {
+    uint32_t w[16];
+    sha::init(out);
+    #pragma unroll
+    for (int i = 0; i < 8; i++) hex2(s[i], w[2 * i], w[2 * i + 1]);
+    shaf::compress_loop(out, w);
+    #pragma unroll
     for (int j = 0; j < 16; j++) w[j] = 0u;
     w[0] = 0x30303030u; w[1] = 0x30303030u;          // "00000000": high u32 of the u64 is 0
     hex2(fv, w[2], w[3]);
     w[4] = 0x80000000u;
-    w[15] = len * 8;
-    shaf::rounds_var(s, w);
-    for (int i = 0; i < 8; i++) st->chan[i] = s[i];
-    st->chan_has = 1;
+    w[15] = 80u * 8u;
+    shaf::compress_loop(out, w);
 }
 
 // ---------------------------------------------------------------- top ----
@@ -295,11 +390,17 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     if (COMMIT && t.k > 0 && !t.st->active[t.k - 1]) return;
     __shared__ uint4 lds[2 * 1024 + 2 * 512];
     __shared__ int32_t red[24];
+    __shared__ uint32_t pre_sh[16];
     const uint32_t L = t.L;
     const uint32_t N = 1u << (L - l);
+    // wave 7 carries the channel prework through the narrow levels
+    const bool pre_wave = COMMIT && threadIdx.x >= 448;
+    ChanPre cp;
+    if (pre_wave) chanpre_init(cp, t.st);
     uint4* A = lds;
     uint4* B = lds + 2 * 1024;
     uint32_t* tr = t.tree;
+    TOP_STAMP(0);
     if (FROM_LEAVES) {
         const size_t half = (size_t)1 << L;
         const uint32_t beta_m = FOLD ? (COMMIT ? t.st->beta_mont[t.k - 1] : t.beta_m) : 0u;
@@ -312,7 +413,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
                 v = t.values[i];
             }
             Dg d;
-            hleaf(v, d);
+            cleaf(v, d);
             dg_store(tr + 8 * i, d);
             dg_lds_store(A + 2 * i, d);
         }
@@ -326,6 +427,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         }
     }
     __syncthreads();
+    TOP_STAMP(1);
     uint32_t cnt = N;
     for (uint32_t lv = l + 1; lv <= L; lv++) {
         cnt >>= 1;
@@ -335,14 +437,22 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
             Dg a, b, o;
             dg_lds_load(A + 4 * q, a);
             dg_lds_load(A + 4 * q + 2, b);
-            hnode(a, b, o);
+            cnode(a, b, o);
             dg_lds_store(B + 2 * q, o);
             dg_store(out + 8 * q, o);
         }
-        __syncthreads();
+        if (pre_wave && cnt <= 448 && cp.step < 3) chanpre_step(cp);
+        lds_barrier();
         uint4* tmp = A; A = B; B = tmp;
+        if (lv - l < 12) TOP_STAMP(1 + lv - l);
     }
     if (!COMMIT) return;
+    if (pre_wave) {
+        while (cp.step < 3) chanpre_step(cp);     // short trees: finish here
+        if (threadIdx.x == 448)
+#pragma unroll
+            for (int i = 0; i < 8; i++) { pre_sh[i] = cp.st[i]; pre_sh[8 + i] = cp.mid[i]; }
+    }
     // ---- degree of poly_k (reference degree field; see DevState) --------
     DevState* st = t.st;
     int m0 = -1, m1 = -1, m2 = -1;
@@ -356,21 +466,29 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     __syncthreads();
     if (threadIdx.x != 0) return;
     for (uint32_t i = 1; i < blockDim.x / 64; i++) { m0 = max(m0, red[3 * i]); m1 = max(m1, red[3 * i + 1]); m2 = max(m2, red[3 * i + 2]); }
+    TOP_STAMP(14);
     const int k = t.k;
     const int deg = (k == 0) ? m0 : (m1 < 0 ? m2 : m0);
     st->deg[k] = deg;
     Dg root;
     dg_lds_load(A, root);
     for (int i = 0; i < 8; i++) st->roots[k][i] = root.w[i];
-    chan_send_root(st, root.w);
+    const uint32_t has = st->chan_has;
+    uint32_t S[8];
+    chan_send_root(has, pre_sh + 8, root.w, S);     // state after send(root_hex)
+    TOP_STAMP(15);
     st->n_layers = (uint32_t)k + 1;
     if (deg >= 1 && k < MAXR && L >= 1) {
-        uint32_t beta = chan_receive_fe(st);
+        uint32_t beta = chan_beta(S);
+        for (int i = 0; i < 8; i++) st->chan[i] = S[i];
+        st->chan_has = 1;
+        st->chan_pending = 1;                        // receive's rehash deferred to the next top
         if (st->forced) beta = st->forced_beta[k];
         st->beta[k] = beta;
         st->beta_mont[k] = to_mont(beta);
         st->active[k] = 1;
         st->n_rounds = (uint32_t)k + 1;
+        TOP_STAMP(16);
     } else {
         st->active[k] = 0;
         if (deg >= 1) { st->status = 7u; return; }            // FRI_EDEGREE
@@ -378,51 +496,81 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         uint32_t fv = (deg == -1) ? 0u : ck[0];
         st->final_value = fv;
         st->final_degree = deg;
-        chan_send_final(st, fv);
+        uint32_t F[8];
+        chan_send_final(S, fv, F);
+        for (int i = 0; i < 8; i++) st->chan[i] = F[i];
+        st->chan_has = 1;
+        st->chan_pending = 0;
     }
 }
 
 // ------------------------------------------------------------ launcher ----
+// Layer schedule (levels are consumed 4 at a time):
+//   L <= 9 : one k_tree_top from the leaves.
+//   L >= 19: k_layer_leaf (1024 leaves/WG -> 64);  11..18: k_layer_leaf_wide (256 -> 16)
+//   then k_tree_mid<1024> while the level has >= 2^18 nodes, k_tree_mid<256>
+//   while it has > 512, and k_tree_top on the last <= 512 nodes.
 void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end) {
     const uint32_t L = t.L;
     const bool fold = t.prev != nullptr;
     const bool commit = t.st != nullptr;
+    const int32_t* nomx = nullptr;
     if (L <= TOP_LOG) {
         if (fold) {
-            if (commit) hipLaunchKernelGGL((k_tree_top<true, true, true>), dim3(1), dim3(512), 0, s, t, 0u, (const int32_t*)nullptr, 1u);
-            else hipLaunchKernelGGL((k_tree_top<true, true, false>), dim3(1), dim3(512), 0, s, t, 0u, (const int32_t*)nullptr, 1u);
+            if (commit) hipLaunchKernelGGL((k_tree_top<true, true, true>), dim3(1), dim3(512), 0, s, t, 0u, nomx, 1u);
+            else hipLaunchKernelGGL((k_tree_top<true, true, false>), dim3(1), dim3(512), 0, s, t, 0u, nomx, 1u);
         } else {
-            if (commit) hipLaunchKernelGGL((k_tree_top<true, false, true>), dim3(1), dim3(512), 0, s, t, 0u, (const int32_t*)nullptr, 1u);
-            else hipLaunchKernelGGL((k_tree_top<true, false, false>), dim3(1), dim3(512), 0, s, t, 0u, (const int32_t*)nullptr, 1u);
+            if (commit) hipLaunchKernelGGL((k_tree_top<true, false, true>), dim3(1), dim3(512), 0, s, t, 0u, nomx, 1u);
+            else hipLaunchKernelGGL((k_tree_top<true, false, false>), dim3(1), dim3(512), 0, s, t, 0u, nomx, 1u);
         }
         if (ev_leaf_end) hipEventRecord(ev_leaf_end, s);
         return;
     }
-    uint32_t G = 1u << (L - 10);
-    if (fold) {
-        if (commit) hipLaunchKernelGGL((k_layer_leaf<true, true>), dim3(G), dim3(256), 0, s, t);
-        else hipLaunchKernelGGL((k_layer_leaf<true, false>), dim3(G), dim3(256), 0, s, t);
+    uint32_t G, out_per_wg;
+    if (L >= 19) {
+        G = 1u << (L - 10);
+        out_per_wg = 64;
+        if (fold) {
+            if (commit) hipLaunchKernelGGL((k_layer_leaf<true, true>), dim3(G), dim3(256), 0, s, t);
+            else hipLaunchKernelGGL((k_layer_leaf<true, false>), dim3(G), dim3(256), 0, s, t);
+        } else {
+            if (commit) hipLaunchKernelGGL((k_layer_leaf<false, true>), dim3(G), dim3(256), 0, s, t);
+            else hipLaunchKernelGGL((k_layer_leaf<false, false>), dim3(G), dim3(256), 0, s, t);
+        }
     } else {
-        if (commit) hipLaunchKernelGGL((k_layer_leaf<false, true>), dim3(G), dim3(256), 0, s, t);
-        else hipLaunchKernelGGL((k_layer_leaf<false, false>), dim3(G), dim3(256), 0, s, t);
+        G = 1u << (L - 8);
+        out_per_wg = 16;
+        if (fold) {
+            if (commit) hipLaunchKernelGGL((k_layer_leaf_wide<true, true>), dim3(G), dim3(256), 0, s, t);
+            else hipLaunchKernelGGL((k_layer_leaf_wide<true, false>), dim3(G), dim3(256), 0, s, t);
+        } else {
+            if (commit) hipLaunchKernelGGL((k_layer_leaf_wide<false, true>), dim3(G), dim3(256), 0, s, t);
+            else hipLaunchKernelGGL((k_layer_leaf_wide<false, false>), dim3(G), dim3(256), 0, s, t);
+        }
     }
     if (ev_leaf_end) hipEventRecord(ev_leaf_end, s);
     const int gate = (commit && t.k > 0) ? t.k - 1 : -1;
-    // coefficient maxima: level 0 at wgmax[0 .. 3G), each mid kernel reduces 16:1
-    int32_t* mx = t.wgmax;
+    // coefficient maxima: level 0 at wgmax[0 .. 3G); each mid reduces R producers per WG
+    const int32_t* mx = commit ? t.wgmax : nullptr;
     size_t mx_off = 3 * (size_t)G;
     uint32_t l = 4;
     while (L - l > TOP_LOG) {
-        const uint32_t grid = 1u << (L - l - 10);
+        const size_t nodes = (size_t)1 << (L - l);
+        const uint32_t nin = nodes >= ((size_t)1 << 18) ? 1024u : 256u;
+        const uint32_t grid = (uint32_t)(nodes / nin);
+        const uint32_t R = nin / out_per_wg;
         int32_t* mx_out = commit ? t.wgmax + mx_off : nullptr;
-        hipLaunchKernelGGL(k_tree_mid, dim3(grid), dim3(512), 0, s, t.tree, L, l, t.st, gate,
-                           commit ? (const int32_t*)mx : (const int32_t*)nullptr, mx_out, G);
+        if (nin == 1024)
+            hipLaunchKernelGGL((k_tree_mid<1024>), dim3(grid), dim3(512), 0, s, t.tree, L, l, t.st, gate, mx, mx_out, R);
+        else
+            hipLaunchKernelGGL((k_tree_mid<256>), dim3(grid), dim3(128), 0, s, t.tree, L, l, t.st, gate, mx, mx_out, R);
         if (commit) { mx = mx_out; mx_off += 3 * (size_t)grid; }
         G = grid;
+        out_per_wg = nin / 16;
         l += 4;
     }
-    if (commit) hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, (const int32_t*)mx, G);
-    else hipLaunchKernelGGL((k_tree_top<false, false, false>), dim3(1), dim3(512), 0, s, t, l, (const int32_t*)nullptr, G);
+    if (commit) hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, mx, G);
+    else hipLaunchKernelGGL((k_tree_top<false, false, false>), dim3(1), dim3(512), 0, s, t, l, nomx, G);
 }
 
 }  // namespace fri

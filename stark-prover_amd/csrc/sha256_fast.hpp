@@ -40,10 +40,10 @@ __device__ __forceinline__ uint32_t s1(uint32_t x) { return xor3(ror(x, 17), ror
 // message: W0 = 0x80000000, W15 = 512, others 0;  KWPAD[t] = K[t] + W[t].
 struct PadKW {
     uint32_t kw[64];
-    constexpr PadKW() : kw() {
+    constexpr PadKW(uint32_t bits = 512u) : kw() {
         uint32_t w[64] = {};
         w[0] = 0x80000000u;
-        w[15] = 512u;
+        w[15] = bits;
         for (int t = 16; t < 64; t++) {
             uint32_t x = w[t - 15], y = w[t - 2];
             uint32_t a = ((x >> 7) | (x << 25)) ^ ((x >> 18) | (x << 14)) ^ (x >> 3);
@@ -63,6 +63,9 @@ struct PadKW {
     }
 };
 constexpr PadKW PAD_KW{};
+// Padding-only final blocks of 128- and 192-byte messages (channel sends).
+__constant__ constexpr PadKW PAD_KW_1024{1024u};
+__constant__ constexpr PadKW PAD_KW_1536{1536u};
 
 // Rounds on a register-resident schedule w[16] (consumed).  Variables are
 // rotated by renaming through the 8-way unrolled macro.
@@ -99,6 +102,80 @@ __device__ __forceinline__ void rounds_pad64(uint32_t st[8]) {
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Rounds with a K+W table in memory (uniform -> scalar loads).
+__device__ __forceinline__ void rounds_kwtab(uint32_t st[8], const uint32_t* kw) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int t = 0; t < 64; t++) {
+        uint32_t t1 = h + kw[t] + S1(e) + chf(e, f, g);
+        uint32_t t2 = S0(a) + majf(a, b, c);
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// ---- compact forms for latency-bound code (executed once per launch, so
+// I-cache footprint matters more than the last few percent of issue rate):
+// 16 rounds unrolled, looped 4x; K and padding schedules via scalar loads.
+__constant__ constexpr uint32_t KTAB[64] = {
+    0x428a2f98u,0x71374491u,0xb5c0fbcfu,0xe9b5dba5u,0x3956c25bu,0x59f111f1u,0x923f82a4u,0xab1c5ed5u,
+    0xd807aa98u,0x12835b01u,0x243185beu,0x550c7dc3u,0x72be5d74u,0x80deb1feu,0x9bdc06a7u,0xc19bf174u,
+    0xe49b69c1u,0xefbe4786u,0x0fc19dc6u,0x240ca1ccu,0x2de92c6fu,0x4a7484aau,0x5cb0a9dcu,0x76f988dau,
+    0x983e5152u,0xa831c66du,0xb00327c8u,0xbf597fc7u,0xc6e00bf3u,0xd5a79147u,0x06ca6351u,0x14292967u,
+    0x27b70a85u,0x2e1b2138u,0x4d2c6dfcu,0x53380d13u,0x650a7354u,0x766a0abbu,0x81c2c92eu,0x92722c85u,
+    0xa2bfe8a1u,0xa81a664bu,0xc24b8b70u,0xc76c51a3u,0xd192e819u,0xd6990624u,0xf40e3585u,0x106aa070u,
+    0x19a4c116u,0x1e376c08u,0x2748774cu,0x34b0bcb5u,0x391c0cb3u,0x4ed8aa4au,0x5b9cca4fu,0x682e6ff3u,
+    0x748f82eeu,0x78a5636fu,0x84c87814u,0x8cc70208u,0x90befffau,0xa4506cebu,0xbef9a3f7u,0xc67178f2u};
+__constant__ constexpr PadKW PAD_KW_C{};
+
+#define SHAF_R(kwv)                                                            \
+    {                                                                          \
+        uint32_t _t1 = h + (kwv) + S1(e) + chf(e, f, g);                        \
+        uint32_t _t2 = S0(a) + majf(a, b, c);                                  \
+        h = g; g = f; f = e; e = d + _t1; d = c; c = b; b = a; a = _t1 + _t2;   \
+    }
+
+__device__ __forceinline__ void compress_loop(uint32_t st[8], uint32_t w[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int i = 0; i < 16; i++) SHAF_R(w[i] + KTAB[i]);
+#pragma unroll 1
+    for (int r = 1; r < 4; r++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            w[i] = w[i] + s0(w[(i + 1) & 15]) + w[(i + 9) & 15] + s1(w[(i + 14) & 15]);
+            SHAF_R(w[i] + KTAB[16 * r + i]);
+        }
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Rounds with a K+W table in constant memory, looped.
+__device__ __forceinline__ void kwtab_loop(uint32_t st[8], const uint32_t* kw) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll 1
+    for (int r = 0; r < 4; r++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) SHAF_R(kw[16 * r + i]);
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+#undef SHAF_R
+
+__device__ __forceinline__ void node_compact(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) { w[i] = l[i]; w[8 + i] = r[i]; }
+    sha::init(out);
+    compress_loop(out, w);
+    kwtab_loop(out, PAD_KW_C.kw);
+}
+__device__ __forceinline__ void leaf_compact(uint32_t v, uint32_t out[8]) {
+    uint32_t w[16] = {0u, v, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 64u};
+    sha::init(out);
+    compress_loop(out, w);
 }
 
 // Leaf: SHA256 of the 8-byte big-endian encoding of a u32 value.

@@ -31,7 +31,7 @@ GENERATOR = 5
 MAX_ROUNDS = 32
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libfri_amd.so"))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", os.environ.get("FRI_AMD_LIB", "libfri_amd.so")))
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "fri_amd.h"))
 
 FRI_OK, FRI_EINVAL, FRI_ENOMEM, FRI_EHIP, FRI_ENODEV, FRI_ERCCL, FRI_ESTATE, FRI_EDEGREE = range(8)
@@ -95,6 +95,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_get_profile": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "fri_reset_profile": (i32, [vp]),
+        "fri_debug_stamps": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), sz]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
