@@ -1,0 +1,124 @@
+"""CPU: the C-ABI library loads and exports every symbol include/fri_amd.h
+declares; the product library carries no oracle code; the host mirror
+(Channel) and bench accounting are consistent with the oracle.  No compute
+calls (no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "stark-prover_amd", "lib", "libfri_amd.so")
+HDR = os.path.join(ROOT, "include", "fri_amd.h")
+
+
+def header_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fri_[a-z_0-9]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib_path():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "stark-prover_amd")], check=True)
+    return LIB
+
+
+def test_header_declares_the_boundary():
+    fns = header_functions()
+    for required in ("fri_ctx_create", "fri_ctx_destroy", "fri_lde", "fri_interpolate", "fri_batch_inverse",
+                     "fri_fold", "fri_merkle_root", "fri_commit", "fri_commit_device", "fri_layer_copy",
+                     "fri_tree_level_copy", "fri_auth_path", "fri_last_error"):
+        assert required in fns
+
+
+def test_header_has_no_torch_or_hip_types():
+    src = re.sub(r"/\*.*?\*/", "", open(HDR).read(), flags=re.S)      # code only, not comments
+    for bad in ("torch", "hipStream_t", "hipEvent_t", "Tensor", "c10::", "#include <hip"):
+        assert bad not in src
+
+
+def test_library_exports_every_declared_symbol(lib_path):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib_path], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+    lib = ctypes.CDLL(lib_path)
+    for f in header_functions():
+        assert getattr(lib, f) is not None
+
+
+def test_product_library_has_no_oracle(lib_path):
+    out = subprocess.run(["nm", "-D", lib_path], capture_output=True, text=True, check=True).stdout
+    assert "orc_" not in out
+    ldd = subprocess.run(["ldd", lib_path], capture_output=True, text=True).stdout
+    assert "oracle" not in ldd
+
+
+def test_version_and_nodev(lib_path):
+    lib = ctypes.CDLL(lib_path)
+    lib.fri_version.restype = ctypes.c_char_p
+    assert b"gfx950" in lib.fri_version()
+    lib.fri_ctx_create.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
+    h = ctypes.c_void_p()
+    assert lib.fri_ctx_create(0, 0, ctypes.byref(h)) == 1          # FRI_EINVAL: log_n_max out of range
+    assert lib.fri_ctx_create(0, 31, ctypes.byref(h)) == 1
+    try:
+        import torch
+        has_gpu = torch.cuda.device_count() > 0
+    except Exception:  # noqa: BLE001
+        has_gpu = False
+    if not has_gpu:
+        assert lib.fri_ctx_create(0, 12, ctypes.byref(h)) == 4     # FRI_ENODEV
+
+
+def test_python_mirror_fails_loudly_without_gpu():
+    import fri_amd
+    try:
+        import torch
+        if torch.cuda.device_count() > 0:
+            pytest.skip("GPU present")
+    except Exception:  # noqa: BLE001
+        pass
+    with pytest.raises(fri_amd.FriError):
+        fri_amd.Context(0, 12)
+
+
+def test_host_channel_mirror_matches_oracle(oracle):
+    import fri_amd
+    a, b = fri_amd.Channel(), oracle.Channel()
+    for msg in (b"", b"abc", bytes(range(64)), b"root" * 16):
+        a.send(msg)
+        b.send(msg)
+        assert a.state == b.state
+        assert a.receive_random_field_element() == b.receive_random_field_element()
+        assert a.receive_random_int(0, 1000, True) == b.receive_random_int(0, 1000, True)
+    assert a.proof == b.proof and a.proof_size() == b.proof_size()
+
+
+def test_host_channel_empty_state_panics():
+    import fri_amd
+    with pytest.raises(fri_amd.FriError):
+        fri_amd.Channel().receive_random_field_element()      # channel.rs:65 expect() on ""
+
+
+def test_canonical_check():
+    import fri_amd
+    with pytest.raises(fri_amd.FriError):
+        fri_amd._u32([fri_amd.P])
+    assert fri_amd._u32([0, fri_amd.P - 1]).dtype.name == "uint32"
+
+
+def test_bench_algorithmic_bytes_match_survey():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    bf, bt = bench.algorithmic_bytes(24, 1 << 21)
+    assert abs((bf + bt) / 1e9 - 2.424) < 0.002                   # 2.424 GB
+    bf, bt = bench.algorithmic_bytes(20, 1 << 17)
+    assert abs((bf + bt) / 1e9 - 0.152) < 0.002
+    assert bench.sha_compressions(24, 1 << 21) > 1.0e8
