@@ -160,6 +160,39 @@ int fri_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level, uint8_t* o
 int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint32_t* value_out,
                   uint8_t* path, uint32_t* depth_out);
 
+/* -------------------------------------------------------------- multi-GPU */
+/* One process per GPU.  A codeword of 2^log_n is committed by G ranks
+ * (G a power of two): rank r computes the coset slice evals[r + G*m] of the
+ * LDE (size n/G NTT), an all-to-all turns it into the contiguous block
+ * [r*n/G, (r+1)*n/G), every layer is hashed block-locally, the G block roots
+ * are all-gathered and the tree top + Fiat-Shamir step run redundantly on
+ * every rank (identical transcript everywhere), and each fold pairs rank
+ * blocks b and b + G/2 (one half-block exchange per layer).  Layers below
+ * 2^20 elements are gathered and finished on every rank. */
+typedef struct {
+    void* user;
+    /* host-staged collectives; buffers are host memory; return 0 on success */
+    int (*allgather)(void* user, const void* send, void* recv, size_t bytes_per_rank);
+    int (*alltoall)(void* user, const void* send, void* recv, size_t bytes_per_peer);
+    int (*sendrecv)(void* user, const void* send, void* recv, size_t bytes, int peer);
+} fri_collectives;
+
+/* RCCL transport (xGMI): rank 0 creates the id, the caller distributes it. */
+int fri_dist_unique_id(uint8_t uid[128]);
+int fri_dist_attach_rccl(fri_ctx* ctx, int rank, int world, const uint8_t uid[128]);
+/* Host-callback transport (e.g. torch.distributed gloo; used by tests). */
+int fri_dist_attach_host(fri_ctx* ctx, int rank, int world, const fri_collectives* ops);
+int fri_dist_detach(fri_ctx* ctx);
+
+/* Sharded fri_commit: every rank passes the same full coefficient vector and
+ * channel state and gets the same result.  world == 1 is fri_commit. */
+int fri_commit_sharded(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n,
+                       uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                       const uint32_t* forced_betas, fri_commit_result* out);
+int fri_commit_sharded_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
+                              uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                              const uint32_t* forced_betas, fri_commit_result* out);
+
 /* ------------------------------------------------------------ diagnostics */
 /* Per-kernel-class device time (ms) accumulated while profiling is enabled
  * (hipEvents recorded on the context's stream around each launch class).

@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/fri_amd.h"
 #include "fri_internal.hpp"
 #include "sha256.hpp"
@@ -39,6 +41,33 @@ struct Plan {
     bool graph_profiled = false;
 };
 
+// Collective transport of the sharded commit: RCCL on the context stream, or
+// host-staged callbacks (synchronous; used by the gloo tests).
+struct Transport {
+    int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;     // main stream collectives
+    ncclComm_t xcomm = nullptr;    // exchange stream (separate communicator: no cross-stream ordering hazard)
+    bool host = false;
+    fri_collectives ops{};
+    uint8_t* hs = nullptr;      // pinned staging
+    uint8_t* hr = nullptr;
+    size_t hcap = 0;
+};
+
+// Scratch of the sharded commit (sized on first use).
+struct DistBuf {
+    size_t cap = 0;             // words in cyc/recv
+    uint32_t* cyc = nullptr;    // coset slice / all-to-all send
+    uint32_t* recv = nullptr;   // all-to-all / gather receive
+    uint32_t* half = nullptr;   // partner half-block
+    uint32_t* roots = nullptr;  // all-gathered block roots (rank order)
+    uint32_t* top = nullptr;    // per-layer top trees (2G digests each)
+    uint32_t* pre_lo = nullptr; // coset pre-scale tables
+    uint32_t* pre_hi = nullptr;
+    size_t gcap = 0;            // words in gath
+    uint32_t* gath = nullptr;   // all-gathered layer at the switch to local
+};
+
 // One timed launch group: events recorded around it on the context stream.
 struct TimedSpan { std::string cls; hipEvent_t b, e; uint64_t bytes; };
 
@@ -64,6 +93,10 @@ struct fri_ctx {
     std::vector<TimedSpan> spans;      // recorded spans of the current commit
     std::vector<hipEvent_t> event_pool;
     size_t event_next = 0;
+    Transport tp;
+    DistBuf db;
+    hipStream_t xstream = nullptr;  // exchange stream (overlaps the local tree)
+    hipEvent_t ev_vals = nullptr, ev_xchg = nullptr;
 };
 
 #define FRI_HIP(ctx, expr)                                                              \
@@ -157,6 +190,8 @@ extern "C" int fri_ctx_create(int device, uint32_t log_n_max, fri_ctx** out) {
     return FRI_OK;
 }
 
+extern "C" int fri_dist_detach(fri_ctx* ctx);
+
 static void plan_free(fri_ctx* ctx) {
     Plan& p = ctx->plan;
     if (p.exec) hipGraphExecDestroy(p.exec);
@@ -172,6 +207,12 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     plan_free(ctx);
     for (auto e : ctx->event_pool) hipEventDestroy(e);
+    fri_dist_detach(ctx);
+    hipFree(ctx->db.cyc); hipFree(ctx->db.recv); hipFree(ctx->db.half); hipFree(ctx->db.roots);
+    hipFree(ctx->db.top); hipFree(ctx->db.pre_lo); hipFree(ctx->db.pre_hi); hipFree(ctx->db.gath);
+    if (ctx->xstream) hipStreamDestroy(ctx->xstream);
+    if (ctx->ev_vals) hipEventDestroy(ctx->ev_vals);
+    if (ctx->ev_xchg) hipEventDestroy(ctx->ev_xchg);
     hipFree(ctx->tw_fwd); hipFree(ctx->tw_inv);
     hipFree(ctx->scratch_a); hipFree(ctx->scratch_b); hipFree(ctx->scratch_c);
     hipFree(ctx->pow_lo); hipFree(ctx->pow_hi);
@@ -652,4 +693,342 @@ extern "C" int fri_reset_profile(fri_ctx* ctx) {
     if (!ctx) return FRI_EINVAL;
     ctx->prof.clear();
     return FRI_OK;
+}
+
+// =================================================================== multi-GPU
+static int tp_host_stage(fri_ctx* ctx, size_t bytes) {
+    Transport& tp = ctx->tp;
+    if (tp.hcap >= bytes) return FRI_OK;
+    if (tp.hs) hipHostFree(tp.hs);
+    if (tp.hr) hipHostFree(tp.hr);
+    tp.hs = tp.hr = nullptr;
+    tp.hcap = 0;
+    FRI_HIP(ctx, hipHostMalloc(&tp.hs, bytes, hipHostMallocDefault));
+    FRI_HIP(ctx, hipHostMalloc(&tp.hr, bytes, hipHostMallocDefault));
+    tp.hcap = bytes;
+    return FRI_OK;
+}
+
+#define FRI_NCCL(ctx, expr)                                                                  \
+    do {                                                                                     \
+        ncclResult_t _r = (expr);                                                            \
+        if (_r != ncclSuccess) {                                                             \
+            (ctx)->err = std::string(#expr) + ": " + ncclGetErrorString(_r);                 \
+            return FRI_ERCCL;                                                                \
+        }                                                                                    \
+    } while (0)
+
+static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
+    Transport& tp = ctx->tp;
+    if (!tp.host) {
+        FRI_NCCL(ctx, ncclAllGather(dsend, drecv, bytes, ncclUint8, tp.comm, s));
+        return FRI_OK;
+    }
+    int rc = tp_host_stage(ctx, bytes * tp.world);
+    if (rc) return rc;
+    FRI_HIP(ctx, hipMemcpyAsync(tp.hs, dsend, bytes, hipMemcpyDeviceToHost, s));
+    FRI_HIP(ctx, hipStreamSynchronize(s));
+    if (tp.ops.allgather(tp.ops.user, tp.hs, tp.hr, bytes)) return fail(ctx, FRI_ERCCL, "allgather callback failed");
+    FRI_HIP(ctx, hipMemcpyAsync(drecv, tp.hr, bytes * tp.world, hipMemcpyHostToDevice, s));
+    return FRI_OK;
+}
+
+static int tp_alltoall(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes_per_peer, hipStream_t s) {
+    Transport& tp = ctx->tp;
+    if (!tp.host) {
+        FRI_NCCL(ctx, ncclGroupStart());
+        for (int p = 0; p < tp.world; p++) {
+            FRI_NCCL(ctx, ncclSend((const uint8_t*)dsend + p * bytes_per_peer, bytes_per_peer, ncclUint8, p, tp.comm, s));
+            FRI_NCCL(ctx, ncclRecv((uint8_t*)drecv + p * bytes_per_peer, bytes_per_peer, ncclUint8, p, tp.comm, s));
+        }
+        FRI_NCCL(ctx, ncclGroupEnd());
+        return FRI_OK;
+    }
+    const size_t tot = bytes_per_peer * tp.world;
+    int rc = tp_host_stage(ctx, tot);
+    if (rc) return rc;
+    FRI_HIP(ctx, hipMemcpyAsync(tp.hs, dsend, tot, hipMemcpyDeviceToHost, s));
+    FRI_HIP(ctx, hipStreamSynchronize(s));
+    if (tp.ops.alltoall(tp.ops.user, tp.hs, tp.hr, bytes_per_peer)) return fail(ctx, FRI_ERCCL, "alltoall callback failed");
+    FRI_HIP(ctx, hipMemcpyAsync(drecv, tp.hr, tot, hipMemcpyHostToDevice, s));
+    return FRI_OK;
+}
+
+static int tp_sendrecv(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, int peer, hipStream_t s) {
+    Transport& tp = ctx->tp;
+    if (!tp.host) {
+        ncclComm_t c = (s == ctx->xstream) ? tp.xcomm : tp.comm;
+        FRI_NCCL(ctx, ncclGroupStart());
+        FRI_NCCL(ctx, ncclSend(dsend, bytes, ncclUint8, peer, c, s));
+        FRI_NCCL(ctx, ncclRecv(drecv, bytes, ncclUint8, peer, c, s));
+        FRI_NCCL(ctx, ncclGroupEnd());
+        return FRI_OK;
+    }
+    int rc = tp_host_stage(ctx, bytes);
+    if (rc) return rc;
+    FRI_HIP(ctx, hipMemcpyAsync(tp.hs, dsend, bytes, hipMemcpyDeviceToHost, s));
+    FRI_HIP(ctx, hipStreamSynchronize(s));
+    if (tp.ops.sendrecv(tp.ops.user, tp.hs, tp.hr, bytes, peer)) return fail(ctx, FRI_ERCCL, "sendrecv callback failed");
+    FRI_HIP(ctx, hipMemcpyAsync(drecv, tp.hr, bytes, hipMemcpyHostToDevice, s));
+    return FRI_OK;
+}
+
+extern "C" int fri_dist_unique_id(uint8_t uid[128]) {
+    if (!uid) return FRI_EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return FRI_ERCCL;
+    memcpy(uid, id.internal, 128);
+    return FRI_OK;
+}
+
+static int dist_check(fri_ctx* ctx, int rank, int world) {
+    if (!ctx || world < 1 || world > 64 || (world & (world - 1)) || rank < 0 || rank >= world)
+        return fail(ctx, FRI_EINVAL, "world must be a power of two <= 64 and 0 <= rank < world");
+    return FRI_OK;
+}
+
+extern "C" int fri_dist_attach_rccl(fri_ctx* ctx, int rank, int world, const uint8_t uid[128]) {
+    int rc = dist_check(ctx, rank, world);
+    if (rc) return rc;
+    if (!uid) return fail(ctx, FRI_EINVAL, "null unique id");
+    fri_dist_detach(ctx);
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    ncclUniqueId id;
+    memcpy(id.internal, uid, 128);
+    FRI_NCCL(ctx, ncclCommInitRank(&ctx->tp.comm, world, id, rank));
+    FRI_NCCL(ctx, ncclCommSplit(ctx->tp.comm, 0, rank, &ctx->tp.xcomm, nullptr));
+    ctx->tp.rank = rank;
+    ctx->tp.world = world;
+    ctx->tp.host = false;
+    return FRI_OK;
+}
+
+extern "C" int fri_dist_attach_host(fri_ctx* ctx, int rank, int world, const fri_collectives* ops) {
+    int rc = dist_check(ctx, rank, world);
+    if (rc) return rc;
+    if (!ops || !ops->allgather || !ops->alltoall || !ops->sendrecv) return fail(ctx, FRI_EINVAL, "null callback");
+    fri_dist_detach(ctx);
+    ctx->tp.rank = rank;
+    ctx->tp.world = world;
+    ctx->tp.host = true;
+    ctx->tp.ops = *ops;
+    return FRI_OK;
+}
+
+extern "C" int fri_dist_detach(fri_ctx* ctx) {
+    if (!ctx) return FRI_EINVAL;
+    Transport& tp = ctx->tp;
+    if (tp.xcomm) ncclCommDestroy(tp.xcomm);
+    if (tp.comm) ncclCommDestroy(tp.comm);
+    if (tp.hs) hipHostFree(tp.hs);
+    if (tp.hr) hipHostFree(tp.hr);
+    tp = Transport();
+    return FRI_OK;
+}
+
+static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
+    DistBuf& b = ctx->db;
+    const size_t nhi = 1u << 20;   // pow table hi part, generous (M <= 2^32)
+    if (b.cap < M) {
+        hipFree(b.cyc); hipFree(b.recv); hipFree(b.half);
+        b.cyc = b.recv = b.half = nullptr;
+        b.cap = 0;
+        FRI_HIP(ctx, hipMalloc(&b.cyc, M * 4));
+        FRI_HIP(ctx, hipMalloc(&b.recv, M * 4));
+        FRI_HIP(ctx, hipMalloc(&b.half, (M / 2 + 1) * 4));
+        b.cap = M;
+    }
+    if (!b.roots) {
+        FRI_HIP(ctx, hipMalloc(&b.roots, 64 * 32));
+        FRI_HIP(ctx, hipMalloc(&b.top, (size_t)(MAXR + 1) * 2 * 64 * 32));
+        FRI_HIP(ctx, hipMalloc(&b.pre_lo, ((size_t)1 << POW_LO_LOG) * 4));
+        FRI_HIP(ctx, hipMalloc(&b.pre_hi, nhi * 4));
+    }
+    if (b.gcap < gwords) {
+        hipFree(b.gath);
+        b.gath = nullptr;
+        FRI_HIP(ctx, hipMalloc(&b.gath, gwords * 4));
+        b.gcap = gwords;
+    }
+    if (!ctx->xstream) {
+        FRI_HIP(ctx, hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking));
+        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_vals, hipEventDisableTiming));
+        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_xchg, hipEventDisableTiming));
+    }
+    (void)G;
+    return FRI_OK;
+}
+
+constexpr uint32_t SHARD_MIN_LOG = 20;   // layers of >= 2^20 elements are hashed sharded
+
+static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
+                              uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                              const uint32_t* forced_betas, fri_commit_result* out) {
+    if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    const uint32_t G = (uint32_t)ctx->tp.world;
+    const uint32_t rank = (uint32_t)ctx->tp.rank;
+    uint32_t logG = 0;
+    while ((1u << logG) < G) logG++;
+    if (G == 1 || log_n < SHARD_MIN_LOG || log_n < logG + 12)
+        return run_commit(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
+    if (log_n > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n out of range for context");
+    const size_t n = (size_t)1 << log_n;
+    if (d > n) return fail(ctx, FRI_EDEGREE, "more coefficients than domain points (domain would be exhausted)");
+    if (offset == 0 || offset >= P) return fail(ctx, FRI_EINVAL, "offset must be a nonzero canonical element");
+    if ((flags & FRI_FLAG_FORCE_BETAS) && !forced_betas) return fail(ctx, FRI_EINVAL, "forced betas missing");
+    if (host_coeffs && !check_canonical(host_coeffs, d)) return fail(ctx, FRI_EINVAL, "coefficient not canonical");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = plan_build(ctx, d, log_n, offset);
+    if (rc) return rc;
+    Plan& p = ctx->plan;
+    hipStream_t s = ctx->stream;
+    const size_t M = n / G;                                   // coset / block size of layer 0
+    rc = dist_buffers(ctx, M, G, (size_t)1 << SHARD_MIN_LOG);
+    if (rc) return rc;
+    DistBuf& db = ctx->db;
+    init_state(ctx, chan_in, flags, forced_betas);
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
+    if (host_coeffs && d)
+        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
+    else if (dev_coeffs && dev_coeffs != p.d_in && d)
+        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, s));
+
+    // ---- layer 0: coset LDE slice evals[rank + G*m] ---------------------
+    const uint32_t sft = mul_std(offset, pow_std(root_of_unity(log_n), rank));   // s = offset * w_n^rank
+    launch_coset_coeffs(p.d_in, d, db.recv, M, pow_std(sft, M), s);              // P mod (x^M - s^M)
+    launch_pow_table(db.pre_lo, db.pre_hi, log_n - logG, sft, 1u, s);
+    NttPlan np{};
+    np.log_n = log_n - logG;
+    np.tw = ctx->tw_fwd;
+    np.pre_lo = db.pre_lo;
+    np.pre_hi = db.pre_hi;
+    launch_ntt(np, db.recv, M, db.cyc, s);
+    rc = tp_alltoall(ctx, db.cyc, db.recv, (M / G) * 4, s);                       // coset slices -> blocks
+    if (rc) return rc;
+    launch_cyclic_to_block(db.recv, p.layers + p.layer_off[0], M, G, s);
+
+    std::vector<uint32_t> block_of(G), rank_of(G);
+    for (uint32_t r = 0; r < G; r++) block_of[r] = rank_of[r] = r;
+    int k = 0;
+    for (;; k++) {
+        const uint32_t Lk = log_n - (uint32_t)k;        // full layer size 2^Lk
+        const size_t B = (size_t)1 << (Lk - logG);       // block size
+        uint32_t* vals = p.layers + p.layer_off[k];     // my block at the start of the layer slot
+        const bool last = (k == p.rmax);
+        const bool next_sharded = !last && (Lk - 1) >= SHARD_MIN_LOG && (Lk - 1 - logG) >= 10;
+        // exchange of the half-block the partner needs for the next fold (overlaps the local tree)
+        const uint32_t b = block_of[rank];
+        const bool isA = b < G / 2;
+        const uint32_t partner = isA ? rank_of[b + G / 2] : rank_of[b - G / 2];
+        if (next_sharded) {
+            if (!ctx->tp.host) {
+                FRI_HIP(ctx, hipEventRecord(ctx->ev_vals, s));
+                FRI_HIP(ctx, hipStreamWaitEvent(ctx->xstream, ctx->ev_vals, 0));
+                rc = tp_sendrecv(ctx, isA ? vals + B / 2 : vals, db.half, (B / 2) * 4, (int)partner, ctx->xstream);
+                if (rc) return rc;
+                FRI_HIP(ctx, hipEventRecord(ctx->ev_xchg, ctx->xstream));
+            } else {
+                rc = tp_sendrecv(ctx, isA ? vals + B / 2 : vals, db.half, (B / 2) * 4, (int)partner, s);
+                if (rc) return rc;
+            }
+        }
+        // block-local tree (levels 0 .. log2 B), gated on round k-1
+        LayerTask tl{};
+        tl.values = vals;
+        tl.tree = p.trees + p.tree_off[k];
+        tl.L = Lk - logG;
+        tl.gst = ctx->d_state;
+        tl.gidx = k > 0 ? k - 1 : -1;
+        launch_layer(tl, s);
+        // all-gather block roots -> block order -> top tree level 0
+        rc = tp_allgather(ctx, tl.tree + 8 * level_offset(tl.L, tl.L), db.roots, 32, s);
+        if (rc) return rc;
+        uint32_t* top = db.top + (size_t)k * 2 * 64 * 8;
+        launch_permute_digests(db.roots, top, G, block_of.data(), s);
+        // coefficient task of this layer (redundant on every rank) + top + channel
+        LayerTask tc{};
+        tc.k = k;
+        tc.coef_in = k ? coef_buf(p, k - 1) : p.d_in;
+        tc.coef_out = k ? coef_buf(p, k) : nullptr;
+        tc.d0 = d;
+        tc.wgmax = p.wgmax;
+        tc.st = ctx->d_state;
+        const size_t clen = k ? ((d + ((size_t)1 << k) - 1) >> k) : d;
+        uint32_t Gc = (uint32_t)((clen + 8191) / 8192);
+        if (Gc < 1) Gc = 1;
+        if (Gc > 2048) Gc = 2048;
+        launch_coef(tc, Gc, s);
+        LayerTask tt = tc;
+        tt.tree = top;
+        tt.L = logG;
+        launch_top(tt, 0, p.wgmax, Gc, s);
+        if (last) break;
+        if (next_sharded) {
+            if (!ctx->tp.host) FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_xchg, 0));
+            const size_t bb = isA ? b : b - G / 2;
+            const uint32_t* first = isA ? vals : db.half;
+            const uint32_t* second = isA ? db.half : vals + B / 2;
+            const uint32_t* xi = p.xinv + p.xinv_off[k] + bb * B + (isA ? 0 : B / 2);
+            launch_pair_fold(first, second, xi, p.layers + p.layer_off[k + 1], B / 2, ctx->d_state, k, s);
+            for (uint32_t r = 0; r < G; r++) {
+                const uint32_t br = block_of[r];
+                block_of[r] = br < G / 2 ? 2 * br : 2 * (br - G / 2) + 1;
+            }
+            for (uint32_t r = 0; r < G; r++) rank_of[block_of[r]] = r;
+            continue;
+        }
+        // switch to local: gather layer k in block order, then the 1-GPU pipeline from k+1
+        rc = tp_allgather(ctx, vals, db.gath, B * 4, s);
+        if (rc) return rc;
+        for (uint32_t r = 0; r < G; r++)
+            FRI_HIP(ctx, hipMemcpyAsync(p.layers + p.layer_off[k] + (size_t)block_of[r] * B, db.gath + (size_t)r * B,
+                                        B * 4, hipMemcpyDeviceToDevice, s));
+        for (int kk = k + 1; kk <= p.rmax; kk++) {
+            LayerTask t{};
+            t.prev = p.layers + p.layer_off[kk - 1];
+            t.xinv = p.xinv + p.xinv_off[kk - 1];
+            t.values = p.layers + p.layer_off[kk];
+            t.tree = p.trees + p.tree_off[kk];
+            t.L = log_n - (uint32_t)kk;
+            t.k = kk;
+            t.coef_in = coef_buf(p, kk - 1);
+            t.coef_out = coef_buf(p, kk);
+            t.d0 = d;
+            t.wgmax = p.wgmax;
+            t.st = ctx->d_state;
+            launch_layer(t, s);
+        }
+        break;
+    }
+    FRI_HIP(ctx, hipGetLastError());
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
+    FRI_HIP(ctx, hipStreamSynchronize(s));
+    const DevState* h = ctx->h_state;
+    if (h->status) return fail(ctx, (int)h->status, "degree exceeds the domain (reference would panic)");
+    memset(out, 0, sizeof *out);
+    out->n_layers = h->n_layers;
+    out->n_rounds = h->n_rounds;
+    out->log_n = log_n;
+    out->final_value = h->final_value;
+    out->final_degree = h->final_degree;
+    for (uint32_t kk = 0; kk < h->n_layers && kk <= (uint32_t)MAXR; kk++) digest_to_bytes(h->roots[kk], out->roots[kk]);
+    for (uint32_t r = 0; r < h->n_rounds && r < (uint32_t)MAXR; r++) out->betas[r] = h->beta[r];
+    digest_to_bytes(h->chan, out->channel_out.digest);
+    out->channel_out.has_state = h->chan_has;
+    ctx->err.clear();
+    return FRI_OK;
+}
+
+extern "C" int fri_commit_sharded(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n, uint32_t offset,
+                                  const fri_channel_state* chan_in, uint32_t flags, const uint32_t* forced_betas,
+                                  fri_commit_result* out) {
+    if (d && !coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    return run_commit_sharded(ctx, coeffs, nullptr, d, log_n, offset, chan_in, flags, forced_betas, out);
+}
+
+extern "C" int fri_commit_sharded_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
+                                         uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                                         const uint32_t* forced_betas, fri_commit_result* out) {
+    if (d && !d_coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    return run_commit_sharded(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
 }

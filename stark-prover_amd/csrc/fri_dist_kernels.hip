@@ -1,0 +1,77 @@
+// fri_dist_kernels.hip — data-layout kernels of the coset-sharded commit
+// (one process per GPU, G ranks).
+//
+//   coset coefficients : rank r evaluates P on the coset s*<w_M>, s = offset*w_n^r,
+//                        M = n/G, via P mod (x^M - s^M) (chunk fold) and a size-M
+//                        NTT with pre-scale s^j  ->  evals[r + G*m], m < M
+//   cyclic -> block     : after the all-to-all, rank g holds chunk t of every
+//                        rank's slice; block[G*t + r] = recv[r][t]
+//   pair fold           : layer k -> k+1 from the local half-block and the
+//                        partner's half-block (fri_commit.rs:53-65)
+//   root permute        : all-gathered block roots, rank order -> block order
+#include "fri_internal.hpp"
+
+namespace fri {
+
+constexpr uint32_t INV2_MD = 0x80000000u;   // Montgomery(2^-1)
+
+// out[j] = sum_t a[j + t*M] * c^t for j < M  (c = s^M, Montgomery c_m).
+__global__ void k_coset_coeffs(const uint32_t* __restrict__ a, size_t d, uint32_t* __restrict__ out, size_t M,
+                               uint32_t c_m) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= M) return;
+    const size_t chunks = (d + M - 1) / M;
+    uint32_t acc = 0;
+    for (size_t t = chunks; t-- > 0;) {
+        const size_t i = j + t * M;
+        acc = add(mmul(acc, c_m), i < d ? a[i] : 0u);
+    }
+    out[j] = acc;
+}
+void launch_coset_coeffs(const uint32_t* a, size_t d, uint32_t* out, size_t M, uint32_t c_std, hipStream_t s) {
+    hipLaunchKernelGGL(k_coset_coeffs, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, a, d, out, M, to_mont(c_std));
+}
+
+// block[G*t + r] = recv[r * (B/G) + t]
+__global__ void k_cyclic_to_block(const uint32_t* __restrict__ recv, uint32_t* __restrict__ block, size_t B, uint32_t G) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const size_t per = B / G;
+    block[i] = recv[(i % G) * per + i / G];
+}
+void launch_cyclic_to_block(const uint32_t* recv, uint32_t* block, size_t B, uint32_t G, hipStream_t s) {
+    hipLaunchKernelGGL(k_cyclic_to_block, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, recv, block, B, G);
+}
+
+// out[j] = fold(first[j], second[j], xinv[j], beta_r), gated on active[r].
+__global__ void k_pair_fold(const uint32_t* __restrict__ first, const uint32_t* __restrict__ second,
+                            const uint32_t* __restrict__ xinv, uint32_t* __restrict__ out, size_t h,
+                            const DevState* __restrict__ st, int r) {
+    if (!st->active[r]) return;
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= h) return;
+    const uint32_t a = first[j], b = second[j];
+    const uint32_t s = add(a, b), t = sub(a, b);
+    out[j] = mmul(add(s, mmul(mmul(t, xinv[j]), st->beta_mont[r])), INV2_MD);
+}
+void launch_pair_fold(const uint32_t* first, const uint32_t* second, const uint32_t* xinv, uint32_t* out, size_t h,
+                      const DevState* st, int r, hipStream_t s) {
+    hipLaunchKernelGGL(k_pair_fold, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, s, first, second, xinv, out, h,
+                       st, r);
+}
+
+struct Perm64 { uint32_t p[64]; };
+// dst digest block_of_rank[r] <- src digest r  (G <= 64)
+__global__ void k_permute_digests(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t G, Perm64 pm) {
+    const uint32_t i = threadIdx.x;        // G * 8 words
+    if (i >= G * 8) return;
+    const uint32_t r = i / 8, w = i % 8;
+    dst[8 * pm.p[r] + w] = src[8 * r + w];
+}
+void launch_permute_digests(const uint32_t* src, uint32_t* dst, uint32_t G, const uint32_t* block_of_rank, hipStream_t s) {
+    Perm64 pm{};
+    for (uint32_t r = 0; r < G && r < 64; r++) pm.p[r] = block_of_rank[r];
+    hipLaunchKernelGGL(k_permute_digests, dim3(1), dim3(512), 0, s, src, dst, G, pm);
+}
+
+}  // namespace fri

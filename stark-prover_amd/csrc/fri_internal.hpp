@@ -88,8 +88,23 @@ struct LayerTask {
     uint32_t* coef_out;        // poly_k coefficients (k >= 1)
     size_t d0;                 // k == 0: input length
     int32_t* wgmax;            // [3 * workgroups] coefficient maxima
-    DevState* st;              // nullptr: standalone Merkle tree
+    DevState* st;              // nullptr: standalone Merkle tree (no degree / channel)
+    const DevState* gst;       // gate for standalone trees inside a commit (sharded
+    int gidx;                  //   layers): skip when !gst->active[gidx]
 };
 void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end = nullptr);
+// Coefficient task of layer t.k alone (grid G): k == 0 scans the input for
+// deg_0, k >= 1 folds poly_{k-1} -> poly_k; maxima into t.wgmax[3*G].
+void launch_coef(const LayerTask& t, uint32_t G, hipStream_t s);
+// fri_dist_kernels.hip
+void launch_coset_coeffs(const uint32_t* a, size_t d, uint32_t* out, size_t M, uint32_t c_std, hipStream_t s);
+void launch_cyclic_to_block(const uint32_t* recv, uint32_t* block, size_t B, uint32_t G, hipStream_t s);
+void launch_pair_fold(const uint32_t* first, const uint32_t* second, const uint32_t* xinv, uint32_t* out, size_t h,
+                      const DevState* st, int r, hipStream_t s);
+void launch_permute_digests(const uint32_t* src, uint32_t* dst, uint32_t G, const uint32_t* block_of_rank,
+                            hipStream_t s);
+// Tree top + degree + channel step for a layer whose level `l` (2^(L-l)
+// nodes, <= 512) is already in t.tree; mx/G: coefficient maxima.
+void launch_top(const LayerTask& t, uint32_t l, const int32_t* mx, uint32_t G, hipStream_t s);
 
 }  // namespace fri

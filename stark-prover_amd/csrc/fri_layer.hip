@@ -157,9 +157,13 @@ __device__ __forceinline__ void lds_two_levels(uint4* lds, const Dg& mine, uint3
     }
 }
 
+__device__ __forceinline__ bool gated_off(const LayerTask& t) {
+    return t.gst && t.gidx >= 0 && !t.gst->active[t.gidx];
+}
+
 template <bool FOLD, bool COMMIT>
 __global__ __launch_bounds__(256) void k_layer_leaf(LayerTask t) {
-    if (COMMIT && FOLD && !t.st->active[t.k - 1]) return;
+    if (gated_off(t)) return;
     __shared__ uint4 lds[512 + 256];
     __shared__ int32_t red[12];
     const uint32_t L = t.L;
@@ -190,7 +194,7 @@ __global__ __launch_bounds__(256) void k_layer_leaf(LayerTask t) {
 // per level): latency 1 leaf + 4 nodes instead of the quad form's 4 + 5.
 template <bool FOLD, bool COMMIT>
 __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
-    if (COMMIT && FOLD && !t.st->active[t.k - 1]) return;
+    if (gated_off(t)) return;
     __shared__ uint4 lds[2 * 256 + 2 * 128];
     __shared__ int32_t red[12];
     const uint32_t L = t.L;
@@ -387,7 +391,7 @@ __device__ __forceinline__ void chan_send_final(const uint32_t s[8], uint32_t fv
 // Otherwise: N = 2^(L-l) <= 1024 level-l digests -> root.
 template <bool FROM_LEAVES, bool FOLD, bool COMMIT>
 __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const int32_t* mx, uint32_t G) {
-    if (COMMIT && t.k > 0 && !t.st->active[t.k - 1]) return;
+    if (gated_off(t)) return;
     __shared__ uint4 lds[2 * 1024 + 2 * 512];
     __shared__ int32_t red[24];
     __shared__ uint32_t pre_sh[16];
@@ -510,7 +514,14 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
 //   L >= 19: k_layer_leaf (1024 leaves/WG -> 64);  11..18: k_layer_leaf_wide (256 -> 16)
 //   then k_tree_mid<1024> while the level has >= 2^18 nodes, k_tree_mid<256>
 //   while it has > 512, and k_tree_top on the last <= 512 nodes.
-void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end) {
+static LayerTask with_gate(const LayerTask& in) {
+    LayerTask t = in;
+    if (t.st) { t.gst = t.st; t.gidx = t.k > 0 ? t.k - 1 : -1; }
+    return t;
+}
+
+void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
+    const LayerTask t = with_gate(tin);
     const uint32_t L = t.L;
     const bool fold = t.prev != nullptr;
     const bool commit = t.st != nullptr;
@@ -549,7 +560,7 @@ void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end) {
         }
     }
     if (ev_leaf_end) hipEventRecord(ev_leaf_end, s);
-    const int gate = (commit && t.k > 0) ? t.k - 1 : -1;
+    const int gate = t.gidx;
     // coefficient maxima: level 0 at wgmax[0 .. 3G); each mid reduces R producers per WG
     const int32_t* mx = commit ? t.wgmax : nullptr;
     size_t mx_off = 3 * (size_t)G;
@@ -561,9 +572,9 @@ void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end) {
         const uint32_t R = nin / out_per_wg;
         int32_t* mx_out = commit ? t.wgmax + mx_off : nullptr;
         if (nin == 1024)
-            hipLaunchKernelGGL((k_tree_mid<1024>), dim3(grid), dim3(512), 0, s, t.tree, L, l, t.st, gate, mx, mx_out, R);
+            hipLaunchKernelGGL((k_tree_mid<1024>), dim3(grid), dim3(512), 0, s, t.tree, L, l, t.gst, gate, mx, mx_out, R);
         else
-            hipLaunchKernelGGL((k_tree_mid<256>), dim3(grid), dim3(128), 0, s, t.tree, L, l, t.st, gate, mx, mx_out, R);
+            hipLaunchKernelGGL((k_tree_mid<256>), dim3(grid), dim3(128), 0, s, t.tree, L, l, t.gst, gate, mx, mx_out, R);
         if (commit) { mx = mx_out; mx_off += 3 * (size_t)grid; }
         G = grid;
         out_per_wg = nin / 16;
@@ -571,6 +582,22 @@ void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end) {
     }
     if (commit) hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, mx, G);
     else hipLaunchKernelGGL((k_tree_top<false, false, false>), dim3(1), dim3(512), 0, s, t, l, nomx, G);
+}
+
+__global__ __launch_bounds__(256) void k_coef(LayerTask t) {
+    if (gated_off(t)) return;
+    __shared__ int32_t red[12];
+    coef_task(t, blockIdx.x, gridDim.x, red);
+}
+
+void launch_coef(const LayerTask& tin, uint32_t G, hipStream_t s) {
+    const LayerTask t = with_gate(tin);
+    hipLaunchKernelGGL(k_coef, dim3(G), dim3(256), 0, s, t);
+}
+
+void launch_top(const LayerTask& tin, uint32_t l, const int32_t* mx, uint32_t G, hipStream_t s) {
+    const LayerTask t = with_gate(tin);
+    hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, mx, G);
 }
 
 }  // namespace fri

@@ -58,6 +58,16 @@ class CommitResult(ctypes.Structure):
                 ("channel_out", ChannelState)]
 
 
+class Collectives(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p),
+                ("allgather", ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_size_t)),
+                ("alltoall", ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_size_t)),
+                ("sendrecv", ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_int))]
+
+
 _lib = None
 
 
@@ -96,6 +106,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "fri_reset_profile": (i32, [vp]),
         "fri_debug_stamps": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), sz]),
+        "fri_dist_unique_id": (i32, [ctypes.c_char_p]),
+        "fri_dist_attach_rccl": (i32, [vp, i32, i32, ctypes.c_char_p]),
+        "fri_dist_attach_host": (i32, [vp, i32, i32, ctypes.POINTER(Collectives)]),
+        "fri_dist_detach": (i32, [vp]),
+        "fri_commit_sharded": (i32, [vp, pu32, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
+                                     ctypes.POINTER(CommitResult)]),
+        "fri_commit_sharded_device": (i32, [vp, vp, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
+                                            ctypes.POINTER(CommitResult)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -224,6 +242,86 @@ class Context:
         dep = ctypes.c_uint32()
         self._check(self.lib.fri_auth_path(self.h, k, index, ctypes.byref(val), buf, ctypes.byref(dep)))
         return val.value, [buf.raw[32 * i: 32 * i + 32] for i in range(dep.value)]
+
+    # ---- multi-GPU ---------------------------------------------------------
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        rc = load_library().fri_dist_unique_id(buf)
+        if rc != FRI_OK:
+            raise FriError(rc, "ncclGetUniqueId failed")
+        return buf.raw
+
+    def attach_rccl(self, rank: int, world: int, uid: bytes):
+        self._check(self.lib.fri_dist_attach_rccl(self.h, rank, world, uid))
+
+    def attach_torch(self, rank: int, world: int):
+        """Host-staged collectives over the default torch.distributed group
+        (gloo on CPU tensors): used to run the sharded path with several
+        ranks on one GPU (tests)."""
+        import torch
+        import torch.distributed as dist
+
+        def as_np(ptr, nbytes):
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), shape=(nbytes,))
+
+        def allgather(user, send, recv, b):
+            try:
+                src = torch.from_numpy(as_np(send, b).copy())
+                outs = [torch.empty(b, dtype=torch.uint8) for _ in range(world)]
+                dist.all_gather(outs, src)
+                dst = as_np(recv, b * world)
+                for r in range(world):
+                    dst[r * b:(r + 1) * b] = outs[r].numpy()
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        def alltoall(user, send, recv, b):
+            try:
+                src = torch.from_numpy(as_np(send, b * world).copy())
+                out = torch.empty(b * world, dtype=torch.uint8)
+                dist.all_to_all_single(out, src)
+                as_np(recv, b * world)[:] = out.numpy()
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        def sendrecv(user, send, recv, b, peer):
+            try:
+                src = torch.from_numpy(as_np(send, b).copy())
+                out = torch.empty(b, dtype=torch.uint8)
+                ops = [dist.P2POp(dist.isend, src, peer), dist.P2POp(dist.irecv, out, peer)]
+                for r in dist.batch_isend_irecv(ops):
+                    r.wait()
+                as_np(recv, b)[:] = out.numpy()
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        t = Collectives._fields_
+        self._cb = Collectives(None, t[1][1](allgather), t[2][1](alltoall), t[3][1](sendrecv))
+        self._check(self.lib.fri_dist_attach_host(self.h, rank, world, ctypes.byref(self._cb)))
+
+    def detach(self):
+        self._check(self.lib.fri_dist_detach(self.h))
+
+    def commit_sharded(self, coeffs, log_n: int, offset: int = GENERATOR, channel_state: Optional[bytes] = None,
+                       forced_betas: Optional[Sequence[int]] = None) -> CommitResult:
+        c = _u32(coeffs)
+        ch = ChannelState()
+        if channel_state:
+            ctypes.memmove(ch.digest, channel_state, 32)
+            ch.has_state = 1
+        flags, fb = 0, None
+        if forced_betas is not None:
+            fb = np.zeros(MAX_ROUNDS, dtype=np.uint32)
+            fb[: len(forced_betas)] = forced_betas
+            flags |= FLAG_FORCE_BETAS
+        res = CommitResult()
+        self._check(self.lib.fri_commit_sharded(self.h, _ptr(c), c.size, log_n, offset, ctypes.byref(ch), flags,
+                                                _ptr(fb) if fb is not None else None, ctypes.byref(res)))
+        return res
 
     def set_profiling(self, on: bool):
         self._check(self.lib.fri_set_profiling(self.h, 1 if on else 0))

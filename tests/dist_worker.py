@@ -1,0 +1,52 @@
+"""Worker for the multi-rank tests (launched by torch.distributed.run, gloo).
+
+    python -m torch.distributed.run --nproc-per-node W --master-addr 127.0.0.1 \
+        --master-port P tests/dist_worker.py MODE LOG_N SEED OUT_DIR
+
+MODE "model": CPU model of the sharded commit (tests/dist_model.py) with the
+              C oracle doing the per-block work and gloo doing the exchanges.
+MODE "gpu":   libfri_amd.so fri_commit_sharded on GPU 0 (every rank shares
+              the one GPU), collectives staged through the host over gloo.
+Each rank writes OUT_DIR/rank<r>.json with its transcript-visible result.
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "stark-prover_amd", "python"))
+sys.path.insert(0, HERE)
+
+
+def main():
+    mode, log_n, seed, out_dir = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    import fri_oracle as fo
+    d = (1 << log_n) // 8
+    coeffs = fo.splitmix64_field(seed, d)
+    if mode == "model":
+        import dist_model
+        res = dist_model.sharded_commit(coeffs, log_n, rank, world, shard_min_log=int(os.environ.get("SHARD_MIN", "8")))
+    else:
+        import fri_amd
+        ctx = fri_amd.Context(0, log_n)
+        ctx.attach_torch(rank, world)
+        r = ctx.commit_sharded(coeffs, log_n)
+        res = {"roots": [bytes(r.roots[k]).hex() for k in range(r.n_layers)],
+               "betas": [int(r.betas[i]) for i in range(r.n_rounds)],
+               "final_value": int(r.final_value), "final_degree": int(r.final_degree),
+               "state": bytes(r.channel_out.digest).hex()}
+        ctx.detach()
+        ctx.close()
+    with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
