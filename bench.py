@@ -10,10 +10,14 @@ random polynomial with d = 2^21 coefficients (blowup 8) onto the codeword
 resident in HBM when the timed region starts, result (roots, betas, final
 value, channel state) read back to the host at the end of every step.
 
-N > 1 (torchrun, one process per GPU): every rank commits its own 2^24
-codeword (weak scaling; the commit of one codeword is a serial Fiat-Shamir
-chain — see DESIGN.md "Multi-GPU").  value = codeword elements committed per
-second summed over ranks, timed by the slowest rank.
+N > 1 (torchrun, one process per GPU): weak scaling, 2^24 codeword elements
+per GPU.  Default --mode sharded: ONE codeword of 2^(24+log2 N) committed
+coset-sharded across the ranks (fri_commit_sharded_device over the library's
+RCCL communicator; BASELINE.json configs[4] at N=8 with --log-n 25).  The
+sharded transcript is checked against each rank's own 1-GPU commit before
+timing; on any mismatch/error every rank falls back to --mode replicas (N
+independent 2^24 commits) and the line carries a "note".  value = codeword
+elements committed per second by the whole job, timed by the slowest rank.
 
 Prints ONE JSON line on rank 0.
 """
@@ -51,13 +55,35 @@ def sha_compressions(log_n, d):
     return leaves + 2 * nodes
 
 
+def _coeffs(seed, d, P):
+    """splitmix64(seed) % p, SURVEY.md §8(d) (same stream as oracle.splitmix64_field)."""
+    import numpy as np
+    idx = np.arange(1, d + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + idx * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z % np.uint64(P)).astype(np.uint32)
+
+
+def _same(a, b):
+    return (a.n_layers == b.n_layers and a.n_rounds == b.n_rounds and a.final_value == b.final_value
+            and a.final_degree == b.final_degree
+            and all(bytes(a.roots[k]) == bytes(b.roots[k]) for k in range(a.n_layers))
+            and list(a.betas)[: a.n_rounds] == list(b.betas)[: b.n_rounds]
+            and bytes(a.channel_out.digest) == bytes(b.channel_out.digest))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--log-n", type=int, default=24)
+    ap.add_argument("--log-n", type=int, default=24, help="codeword log2 per GPU (weak scaling)")
     ap.add_argument("--blowup-log", type=int, default=3)
+    ap.add_argument("--mode", choices=("sharded", "replicas"), default="sharded",
+                    help="N>1: one coset-sharded codeword of 2^(log_n+log2 N) (default), or N independent commits")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -70,38 +96,63 @@ def main():
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        # control plane (unique-id broadcast, barriers, max-over-ranks) on gloo;
+        # the data path runs on the library's own RCCL communicator.
+        dist.init_process_group("gloo")
 
     import numpy as np
     import fri_amd
 
-    log_n = args.log_n
+    logG = world.bit_length() - 1
+    mode = args.mode if world > 1 else "single"
+    if world > 1 and (1 << logG) != world:
+        mode = "replicas"                                   # sharding needs a power-of-two world
+    log_n = args.log_n + (logG if mode == "sharded" else 0)   # codeword committed by the job (sharded) / rank
     d = 1 << (log_n - args.blowup_log)
     ctx = fri_amd.Context(local_rank if world > 1 else 0, log_n)
+    note = None
 
-    # synthetic coefficients: splitmix64(seed) % p, seed per rank
-    seed = 42 + rank
-    mask = (1 << 64) - 1
-    x = np.uint64(seed)
-    idx = np.arange(1, d + 1, dtype=np.uint64)
-    with np.errstate(over="ignore"):
-        z = np.uint64(seed) + idx * np.uint64(0x9E3779B97F4A7C15)
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        z = z ^ (z >> np.uint64(31))
-    coeffs = (z % np.uint64(fri_amd.P)).astype(np.uint32)
-    del x, mask
+    if mode == "sharded":
+        import torch
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            uid = torch.frombuffer(bytearray(fri_amd.Context.unique_id()), dtype=torch.uint8).clone()
+        dist.broadcast(uid, 0)
+        coeffs = _coeffs(42, d, fri_amd.P)                    # one polynomial for the whole job
+        ok = 1
+        try:
+            ctx.attach_rccl(rank, world, bytes(uid.numpy()))
+            res0 = ctx.commit_sharded(coeffs, log_n)
+            # check the sharded transcript against this rank's own 1-GPU commit of the same codeword
+            ok = int(_same(res0, ctx.commit(coeffs, log_n)))
+        except fri_amd.FriError as e:
+            ok, note = 0, f"sharded path failed: {e}"
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            note = note or "sharded transcript differed from the 1-GPU commit"
+            print(f"[bench] rank {rank}: {note}; falling back to replicas", file=sys.stderr, flush=True)
+            try:
+                ctx.detach()
+            except fri_amd.FriError:
+                pass
+            ctx.close()
+            mode = "replicas"
+            log_n = args.log_n
+            d = 1 << (log_n - args.blowup_log)
+            ctx = fri_amd.Context(local_rank, log_n)
+    if mode != "sharded":
+        coeffs = _coeffs(42 + rank, d, fri_amd.P)             # replicas: an independent codeword per rank
+        res0 = ctx.commit(coeffs, log_n)
 
-    # build the plan and place the input in the context's device buffer (untimed)
-    res0 = ctx.commit(coeffs, log_n)
+    # inputs resident in HBM: the plan's input buffer, filled by the untimed first commit
     dptr = ctypes.c_void_p()
     ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(dptr)))
     res = fri_amd.CommitResult()
+    entry = ctx.lib.fri_commit_sharded_device if mode == "sharded" else ctx.lib.fri_commit_device
 
     def step():
-        rc = ctx.lib.fri_commit_device(ctx.h, dptr, d, log_n, fri_amd.GENERATOR, None, 0, None,
-                                       ctypes.byref(res))
-        ctx._check(rc)
+        ctx._check(entry(ctx.h, dptr, d, log_n, fri_amd.GENERATOR, None, 0, None, ctypes.byref(res)))
 
     def barrier_sync():
         if dist is not None:
@@ -112,7 +163,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    assert bytes(res.roots[0]) == bytes(res0.roots[0])
+    if args.warmup:
+        assert _same(res, res0)
 
     barrier_sync()
     t0 = time.perf_counter()
@@ -122,13 +174,15 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     n = 1 << log_n
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = world * n * args.steps / elapsed
+    units_per_step = n if mode == "sharded" else world * n
+    value = units_per_step * args.steps / elapsed
+    blk_log = log_n - (logG if mode == "sharded" else 0)     # layer-0 elements hashed by one GPU
 
     # ---- roofline of the dominant kernel: HIP events on the context stream,
     # recorded around every launch of that kernel during profiled steps.
@@ -155,18 +209,18 @@ def main():
             # (DESIGN.md "VALU cost model"): leaf hash 2009 issue units, node
             # hash 3592 (v_alignbit/v_add3 are half rate on gfx950).  The leaf
             # kernel hashes 2^L leaves and (15/16) 2^L nodes (levels 1..4).
-            nleaf = 1 << log_n
+            nleaf = 1 << blk_log
             units = nleaf * 2009.0 + (15.0 / 16.0) * nleaf * 3592.0
             roofline["valu"] = {"issue_units_per_launch": units,
                                 "achieved_T_units_s": round(units / (avg_ms * 1e-3) / 1e12, 2),
                                 "peak_T_units_s": VALU_PEAK_TOPS,
                                 "frac": round(units / (avg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
         breakdown = {}
-        for cls in ("lde", "merkle_layer0_leaf", "layer0", "layers"):
+        for cls in ("lde", "alltoall", "merkle_layer0_leaf", "layer0", "layers", "gather"):
             cms, cl, _ = ctx.profile(cls)
             if cl:
                 breakdown[cls] = round(cms / prof_steps, 4)
-        traffic = _pmc_traffic(log_n)
+        traffic = _pmc_traffic(blk_log)
         if roofline is not None and traffic is not None:
             roofline["traffic"] = traffic
 
@@ -181,22 +235,32 @@ def main():
         cpu = _cpu_baseline(coeffs, d, log_n)
 
     if rank == 0:
+        if mode == "sharded":
+            workload = (f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} (d=2^{log_n - args.blowup_log}), "
+                        f"coset-sharded over {world} GPUs (2^{blk_log} per GPU), SHA-256 Merkle per layer, "
+                        f"{res.n_rounds} rounds")
+            par = f"coset-sharded x{world} (RCCL all-to-all + pair exchange)"
+        else:
+            workload = (f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} (d=2^{log_n - args.blowup_log}), "
+                        f"SHA-256 Merkle per layer, {res.n_rounds} rounds" + (", per GPU" if world > 1 else ""))
+            par = f"replicas x{world}" if world > 1 else "single GPU"
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "field-elems/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (splitmix64 % p coefficients, seed 42+rank)",
-            "config": {"workload": f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} "
-                                   f"(d=2^{log_n - args.blowup_log}), SHA-256 Merkle per layer, "
-                                   f"{res.n_rounds} rounds, per GPU",
-                       "codeword_log2": log_n, "blowup": 1 << args.blowup_log, "field": "p=3*2^30+1",
-                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+            "data": "synthetic (splitmix64 % p coefficients" + (", seed 42)" if mode != "replicas" else ", seed 42+rank)"),
+            "config": {"workload": workload, "codeword_log2": log_n, "per_gpu_log2": blk_log,
+                       "blowup": 1 << args.blowup_log, "field": "p=3*2^30+1", "parallelism": par},
             "roofline": roofline,
             "whole_commit": whole,
             "breakdown_ms_per_step": breakdown,
             "cpu_baseline": cpu,
         }
+        if note:
+            line["note"] = note
         print(json.dumps(line), flush=True)
+    if mode == "sharded":
+        ctx.detach()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

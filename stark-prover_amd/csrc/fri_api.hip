@@ -795,8 +795,15 @@ extern "C" int fri_dist_attach_rccl(fri_ctx* ctx, int rank, int world, const uin
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     ncclUniqueId id;
     memcpy(id.internal, uid, 128);
-    FRI_NCCL(ctx, ncclCommInitRank(&ctx->tp.comm, world, id, rank));
-    FRI_NCCL(ctx, ncclCommSplit(ctx->tp.comm, 0, rank, &ctx->tp.xcomm, nullptr));
+    ncclComm_t comm = nullptr, xcomm = nullptr;
+    FRI_NCCL(ctx, ncclCommInitRank(&comm, world, id, rank));
+    ncclResult_t r = ncclCommSplit(comm, 0, rank, &xcomm, nullptr);   // second comm for the exchange stream
+    if (r != ncclSuccess) {
+        ncclCommDestroy(comm);
+        return fail(ctx, FRI_ERCCL, std::string("ncclCommSplit: ") + ncclGetErrorString(r));
+    }
+    ctx->tp.comm = comm;
+    ctx->tp.xcomm = xcomm;
     ctx->tp.rank = rank;
     ctx->tp.world = world;
     ctx->tp.host = false;
@@ -895,6 +902,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
 
     // ---- layer 0: coset LDE slice evals[rank + G*m] ---------------------
     const uint32_t sft = mul_std(offset, pow_std(root_of_unity(log_n), rank));   // s = offset * w_n^rank
+    size_t sp = span_begin(ctx, "lde", d * 4 + M * 8);
     launch_coset_coeffs(p.d_in, d, db.recv, M, pow_std(sft, M), s);              // P mod (x^M - s^M)
     launch_pow_table(db.pre_lo, db.pre_hi, log_n - logG, sft, 1u, s);
     NttPlan np{};
@@ -903,9 +911,12 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     np.pre_lo = db.pre_lo;
     np.pre_hi = db.pre_hi;
     launch_ntt(np, db.recv, M, db.cyc, s);
+    span_end(ctx, sp);
+    sp = span_begin(ctx, "alltoall", M * 4);
     rc = tp_alltoall(ctx, db.cyc, db.recv, (M / G) * 4, s);                       // coset slices -> blocks
     if (rc) return rc;
     launch_cyclic_to_block(db.recv, p.layers + p.layer_off[0], M, G, s);
+    span_end(ctx, sp);
 
     std::vector<uint32_t> block_of(G), rank_of(G);
     for (uint32_t r = 0; r < G; r++) block_of[r] = rank_of[r] = r;
@@ -939,7 +950,12 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         tl.L = Lk - logG;
         tl.gst = ctx->d_state;
         tl.gidx = k > 0 ? k - 1 : -1;
-        launch_layer(tl, s);
+        uint64_t leaf_nodes = 0;
+        for (uint32_t j = 0; j <= 4 && j <= tl.L; j++) leaf_nodes += (uint64_t)1 << (tl.L - j);
+        size_t spl = (k == 0 && tl.L >= 19) ? span_begin(ctx, "merkle_layer0_leaf", ((uint64_t)4 << tl.L) + 32 * leaf_nodes)
+                                            : (size_t)-1;
+        size_t spk = span_begin(ctx, k == 0 ? "layer0" : "layers", 0);
+        launch_layer(tl, s, spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
         // all-gather block roots -> block order -> top tree level 0
         rc = tp_allgather(ctx, tl.tree + 8 * level_offset(tl.L, tl.L), db.roots, 32, s);
         if (rc) return rc;
@@ -962,6 +978,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         tt.tree = top;
         tt.L = logG;
         launch_top(tt, 0, p.wgmax, Gc, s);
+        span_end(ctx, spk);
         if (last) break;
         if (next_sharded) {
             if (!ctx->tp.host) FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_xchg, 0));
@@ -978,6 +995,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
             continue;
         }
         // switch to local: gather layer k in block order, then the 1-GPU pipeline from k+1
+        sp = span_begin(ctx, "gather", B * 4 * G);
         rc = tp_allgather(ctx, vals, db.gath, B * 4, s);
         if (rc) return rc;
         for (uint32_t r = 0; r < G; r++)
@@ -998,11 +1016,13 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
             t.st = ctx->d_state;
             launch_layer(t, s);
         }
+        span_end(ctx, sp);
         break;
     }
     FRI_HIP(ctx, hipGetLastError());
     FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
     FRI_HIP(ctx, hipStreamSynchronize(s));
+    if (ctx->profiling) spans_collect(ctx);
     const DevState* h = ctx->h_state;
     if (h->status) return fail(ctx, (int)h->status, "degree exceeds the domain (reference would panic)");
     memset(out, 0, sizeof *out);

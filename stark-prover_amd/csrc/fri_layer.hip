@@ -251,7 +251,7 @@ __device__ __forceinline__ void reduce_mx(const int32_t* in, int32_t* out, uint3
 template <uint32_t NIN>
 __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st,
                                                       int gate, const int32_t* mx_in, int32_t* mx_out, uint32_t R) {
-    if (gate >= 0 && !st->active[gate]) return;
+    if (st && gate >= 0 && !st->active[gate]) return;
     __shared__ uint4 lds[2 * NIN + NIN];
     uint4* A = lds;
     uint4* B = lds + 2 * NIN;
