@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--blowup-log", type=int, default=3)
     ap.add_argument("--mode", choices=("sharded", "replicas"), default="sharded",
                     help="N>1: one coset-sharded codeword of 2^(log_n+log2 N) (default), or N independent commits")
+    ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
+                    help="sharded data path: the library's RCCL communicator, or host-staged gloo (rehearsal only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -92,10 +94,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local_rank
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
+        ndev = torch.cuda.device_count()          # does not initialise HIP
+        device = local_rank % max(ndev, 1)        # rehearsal with more ranks than GPUs shares devices
+        torch.cuda.set_device(device)
         # control plane (unique-id broadcast, barriers, max-over-ranks) on gloo;
         # the data path runs on the library's own RCCL communicator.
         dist.init_process_group("gloo")
@@ -109,7 +114,7 @@ def main():
         mode = "replicas"                                   # sharding needs a power-of-two world
     log_n = args.log_n + (logG if mode == "sharded" else 0)   # codeword committed by the job (sharded) / rank
     d = 1 << (log_n - args.blowup_log)
-    ctx = fri_amd.Context(local_rank if world > 1 else 0, log_n)
+    ctx = fri_amd.Context(device, log_n)
     note = None
 
     if mode == "sharded":
@@ -121,7 +126,10 @@ def main():
         coeffs = _coeffs(42, d, fri_amd.P)                    # one polynomial for the whole job
         ok = 1
         try:
-            ctx.attach_rccl(rank, world, bytes(uid.numpy()))
+            if args.transport == "host":
+                ctx.attach_torch(rank, world)
+            else:
+                ctx.attach_rccl(rank, world, bytes(uid.numpy()))
             res0 = ctx.commit_sharded(coeffs, log_n)
             # check the sharded transcript against this rank's own 1-GPU commit of the same codeword
             ok = int(_same(res0, ctx.commit(coeffs, log_n)))
@@ -140,7 +148,7 @@ def main():
             mode = "replicas"
             log_n = args.log_n
             d = 1 << (log_n - args.blowup_log)
-            ctx = fri_amd.Context(local_rank, log_n)
+            ctx = fri_amd.Context(device, log_n)
     if mode != "sharded":
         coeffs = _coeffs(42 + rank, d, fri_amd.P)             # replicas: an independent codeword per rank
         res0 = ctx.commit(coeffs, log_n)
@@ -239,7 +247,8 @@ def main():
             workload = (f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} (d=2^{log_n - args.blowup_log}), "
                         f"coset-sharded over {world} GPUs (2^{blk_log} per GPU), SHA-256 Merkle per layer, "
                         f"{res.n_rounds} rounds")
-            par = f"coset-sharded x{world} (RCCL all-to-all + pair exchange)"
+            par = (f"coset-sharded x{world} (RCCL all-to-all + pair exchange)" if args.transport == "rccl"
+                   else f"coset-sharded x{world} (host-staged gloo transport, rehearsal)")
         else:
             workload = (f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} (d=2^{log_n - args.blowup_log}), "
                         f"SHA-256 Merkle per layer, {res.n_rounds} rounds" + (", per GPU" if world > 1 else ""))
