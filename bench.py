@@ -238,6 +238,16 @@ def main():
              "frac_of_hbm_peak": round((b_field + b_tree) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
              "sha256_compressions": sha_compressions(log_n, d)}
 
+    # PCIe-inclusive rate (host coefficients in, result out): never `value`
+    pcie = None
+    if world == 1:
+        k = max(3, min(args.steps, 10))
+        t0 = time.perf_counter()
+        for _ in range(k):
+            ctx.commit(coeffs, log_n)
+        pcie = {"ms_per_step": round(1000.0 * (time.perf_counter() - t0) / k, 4),
+                "what": f"fri_commit from a pageable host buffer of {d} u32 coefficients (H2D inside the call)"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = _cpu_baseline(coeffs, d, log_n)
@@ -263,6 +273,7 @@ def main():
             "roofline": roofline,
             "whole_commit": whole,
             "breakdown_ms_per_step": breakdown,
+            "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
         }
         if note:

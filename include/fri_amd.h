@@ -185,7 +185,10 @@ int fri_dist_attach_host(fri_ctx* ctx, int rank, int world, const fri_collective
 int fri_dist_detach(fri_ctx* ctx);
 
 /* Sharded fri_commit: every rank passes the same full coefficient vector and
- * channel state and gets the same result.  world == 1 is fri_commit. */
+ * channel state and gets the same result.  world == 1 is fri_commit.
+ * Afterwards fri_layer_copy / fri_tree_level_copy / fri_auth_path serve the
+ * layers finished on every rank (the < 2^20 tail); the sharded layers return
+ * FRI_ESTATE (each rank holds only its block). */
 int fri_commit_sharded(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n,
                        uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                        const uint32_t* forced_betas, fri_commit_result* out);
@@ -194,9 +197,12 @@ int fri_commit_sharded_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, 
                               const uint32_t* forced_betas, fri_commit_result* out);
 
 /* ------------------------------------------------------------ diagnostics */
-/* Per-kernel-class device time (ms) accumulated while profiling is enabled
- * (hipEvents recorded on the context's stream around each launch class).
- * names: "lde", "merkle_leaf", "merkle_node", "fold", "coeff_fold", "channel". */
+/* Per-span device time (ms) accumulated while profiling is enabled (hipEvents
+ * recorded on the context's stream; profiling commits run eagerly, no graph).
+ * Classes: "lde" (LDE NTT), "merkle_layer0_leaf" (layer-0 leaf kernel: leaves
+ * + levels 1-4, with its algorithmic bytes), "layer0" (all of layer 0's tree +
+ * channel step), "layers" (layers >= 1), and for sharded commits "alltoall"
+ * and "gather".  bytes = algorithmic bytes of the span where defined. */
 int fri_set_profiling(fri_ctx* ctx, int enabled);
 int fri_get_profile(fri_ctx* ctx, const char* kernel_class, double* total_ms, uint64_t* launches,
                     uint64_t* bytes);

@@ -97,6 +97,7 @@ struct fri_ctx {
     DistBuf db;
     hipStream_t xstream = nullptr;  // exchange stream (overlaps the local tree)
     hipEvent_t ev_vals = nullptr, ev_xchg = nullptr;
+    uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
 };
 
 #define FRI_HIP(ctx, expr)                                                              \
@@ -546,6 +547,7 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
     if (rc) return rc;
     Plan& p = ctx->plan;
     hipStream_t s = ctx->stream;
+    ctx->sharded_layers = 0;
     init_state(ctx, chan_in, flags, forced_betas);
     FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
     if (host_coeffs && d)
@@ -614,6 +616,8 @@ extern "C" int fri_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out, size_
     if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
     const Plan& p = ctx->plan;
     if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
+    if (layer < ctx->sharded_layers)
+        return fail(ctx, FRI_ESTATE, "layer was committed sharded: this rank holds only its block (fri_commit_sharded)");
     size_t m = (size_t)1 << (p.log_n - layer);
     if (cap < m) return fail(ctx, FRI_EINVAL, "output buffer too small");
     FRI_HIP(ctx, hipMemcpy(out, p.layers + p.layer_off[layer], m * 4, hipMemcpyDeviceToHost));
@@ -624,6 +628,8 @@ extern "C" int fri_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level,
     if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
     const Plan& p = ctx->plan;
     if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
+    if (layer < ctx->sharded_layers)
+        return fail(ctx, FRI_ESTATE, "layer was committed sharded: this rank holds only its block (fri_commit_sharded)");
     uint32_t L = p.log_n - layer;
     if (level > L) return fail(ctx, FRI_EINVAL, "level above root");
     size_t cnt = (size_t)1 << (L - level);
@@ -640,6 +646,8 @@ extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint3
     if (!ctx || !value_out || !depth_out) return fail(ctx, FRI_EINVAL, "null argument");
     const Plan& p = ctx->plan;
     if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
+    if (layer < ctx->sharded_layers)
+        return fail(ctx, FRI_ESTATE, "layer was committed sharded: this rank holds only its block (fri_commit_sharded)");
     uint32_t L = p.log_n - layer;
     if (index >> L) return fail(ctx, FRI_EINVAL, "index out of range");
     FRI_HIP(ctx, hipMemcpy(value_out, p.layers + p.layer_off[layer] + index, 4, hipMemcpyDeviceToHost));
@@ -893,6 +901,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     rc = dist_buffers(ctx, M, G, (size_t)1 << SHARD_MIN_LOG);
     if (rc) return rc;
     DistBuf& db = ctx->db;
+    ctx->sharded_layers = (uint32_t)p.rmax + 1;      // lowered when the tail goes local
     init_state(ctx, chan_in, flags, forced_betas);
     FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
     if (host_coeffs && d)
@@ -995,6 +1004,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
             continue;
         }
         // switch to local: gather layer k in block order, then the 1-GPU pipeline from k+1
+        ctx->sharded_layers = (uint32_t)k + 1;   // layer k keeps its block-local tree; k+1.. are local
         sp = span_begin(ctx, "gather", B * 4 * G);
         rc = tp_allgather(ctx, vals, db.gath, B * 4, s);
         if (rc) return rc;

@@ -25,6 +25,8 @@ def main():
     import torch.distributed as dist
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
+    import numpy as np
+
     import fri_oracle as fo
     d = (1 << log_n) // 8
     coeffs = fo.splitmix64_field(seed, d)
@@ -40,7 +42,20 @@ def main():
                "betas": [int(r.betas[i]) for i in range(r.n_rounds)],
                "final_value": int(r.final_value), "final_degree": int(r.final_degree),
                "state": bytes(r.channel_out.digest).hex()}
+        # read-back: sharded layers are refused, the locally finished tail is served
+        try:
+            ctx.layer(0, log_n)
+            res["layer0_refused"] = False
+        except fri_amd.FriError:
+            res["layer0_refused"] = True
+        last = r.n_layers - 1
+        tail = ctx.layer(last, log_n)
+        _, path = ctx.auth_path(last, 1, log_n)
         ctx.detach()
+        single = ctx.commit(coeffs, log_n)
+        res["tail_matches_single"] = bool(np.array_equal(tail, ctx.layer(last, log_n)))
+        res["auth_matches_single"] = path == ctx.auth_path(last, 1, log_n)[1]
+        res["single_root0"] = bytes(single.roots[0]).hex()
         ctx.close()
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
         json.dump(res, f)

@@ -76,3 +76,5 @@ def test_sharded_commit_gpu_matches_single(world, corc, oracle):
         assert r["betas"] == [ores.betas[i] for i in range(ores.n_rounds)]
         assert r["final_value"] == ores.final_value
         assert r["state"] == och.state.decode()
+        assert r["layer0_refused"] and r["tail_matches_single"] and r["auth_matches_single"]
+        assert r["single_root0"] == want_roots[0]
