@@ -160,6 +160,17 @@ int fri_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level, uint8_t* o
 int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint32_t* value_out,
                   uint8_t* path, uint32_t* depth_out);
 
+/* Decommitment of one FRI query (decommit_fri_layers, src/fri/fri_commit.rs:
+ * 137-163) from the layers and trees of the last fri_commit, still in HBM.
+ * For every committed layer k (m_k = 2^(log_n-k) elements): idx = index % m_k,
+ * sib = (idx + m_k/2) % m_k; values[2k] = layer_k[idx], values[2k+1] =
+ * layer_k[sib]; paths = for each k, the authentication path of idx then of
+ * sib (rs_merkle single-leaf proof: sibling digests leaf -> root, 32 bytes
+ * each, (log_n-k) per path) — the byte strings the reference sends.
+ * *paths_len = total path bytes (also set when paths_cap is too small). */
+int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap,
+                       uint8_t* paths, size_t paths_cap, size_t* paths_len);
+
 /* -------------------------------------------------------------- multi-GPU */
 /* One process per GPU.  A codeword of 2^log_n is committed by G ranks
  * (G a power of two): rank r computes the coset slice evals[r + G*m] of the

@@ -230,6 +230,21 @@ def merkle_root_hex(values: Sequence[int]) -> str:     # mod.rs:24-26
     return merkle_levels(values)[-1][0].hex()
 
 
+def merkle_proof(levels: List[List[bytes]], idx: int) -> bytes:
+    """Authentication path of leaf `idx` as the bytes the decommitment sends
+    (fri_commit.rs:155,159 `get_authentication_path`): the
+    rs_merkle 1.4.2 single-leaf proof, sibling hashes leaf -> root, a level
+    whose node has no sibling (odd promotion) contributing nothing.
+    Parity unpinned: the wrapper in src/merkle/mod.rs has no such method."""
+    out = b""
+    for lvl in levels[:-1]:
+        sib = idx ^ 1
+        if sib < len(lvl):
+            out += lvl[sib]
+        idx >>= 1
+    return out
+
+
 # --------------------------------------------------------------------------
 # Channel — src/channel/channel.rs
 # --------------------------------------------------------------------------
@@ -330,6 +345,28 @@ def fri_commit(coeffs: Sequence[int], log_n: int, channel: Channel, offset: int 
     final = 0 if deg == -1 else poly[0]                              # :109-113
     channel.send(fe_to_bytes(final))                                 # :114
     return FriResult(roots, betas, final, deg, layers, trees)
+
+
+def decommit_fri_layers(index: int, layers, trees, channel: Channel) -> None:
+    """fri_commit.rs:137-163, including its quirk: a 1-element layer sends
+    its value and then still sends value/path/sibling/path (idx = sib = 0)."""
+    for evals, levels in zip(layers, trees):
+        length = len(evals)
+        if length == 1:
+            channel.send(fe_to_bytes(evals[0]))
+        idx = index % length
+        sib = (idx + length // 2) % length
+        channel.send(fe_to_bytes(evals[idx]))
+        channel.send(merkle_proof(levels, idx))
+        channel.send(fe_to_bytes(evals[sib]))
+        channel.send(merkle_proof(levels, sib))
+
+
+def decommit_fri(num_queries: int, max_index: int, layers, trees, channel: Channel) -> None:
+    """fri_commit.rs:168-179: each query index is drawn from the transcript."""
+    for _ in range(num_queries):
+        idx = channel.receive_random_int(0, max_index, True)
+        decommit_fri_layers(idx, layers, trees, channel)
 
 
 def splitmix64_field(seed: int, count: int, M: int = P) -> List[int]:

@@ -18,8 +18,12 @@ for _ in range(3):
 buf = (ctypes.c_uint64 * (33 * 24))()
 ctx._check(ctx.lib.fri_debug_stamps(ctx.h, buf, 33 * 24))
 a = np.frombuffer(buf, dtype=np.uint64).reshape(33, 24).astype(np.int64)
+prev_end = 0
 for k in range(res.n_layers):
     row = a[k]
     t0 = row[0]
     marks = [(i, (row[i] - t0) / 100.0) for i in range(1, 24) if row[i] > 0]
-    print(f"layer {k:2d} L={log_n - k:2d}: " + " ".join(f"{i}:{us:.1f}" for i, us in marks))
+    last = max(row[i] for i in range(24))
+    gap = (t0 - prev_end) / 100.0 if k else 0.0
+    prev_end = last
+    print(f"layer {k:2d} L={log_n - k:2d} since-prev-top={gap:6.1f}: " + " ".join(f"{i}:{us:.1f}" for i, us in marks))

@@ -98,6 +98,7 @@ struct fri_ctx {
     hipStream_t xstream = nullptr;  // exchange stream (overlaps the local tree)
     hipEvent_t ev_vals = nullptr, ev_xchg = nullptr;
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
+    uint32_t* dq_buf = nullptr;     // decommitment gather staging (64 KiB)
 };
 
 #define FRI_HIP(ctx, expr)                                                              \
@@ -218,6 +219,7 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     hipFree(ctx->scratch_a); hipFree(ctx->scratch_b); hipFree(ctx->scratch_c);
     hipFree(ctx->pow_lo); hipFree(ctx->pow_hi);
     hipFree(ctx->d_state);
+    hipFree(ctx->dq_buf);
     if (ctx->h_state) hipHostFree(ctx->h_state);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -659,6 +661,41 @@ extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint3
         digest_to_bytes(w, path + 32 * l);
     }
     *depth_out = L;
+    return FRI_OK;
+}
+
+extern "C" int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap,
+                                  uint8_t* paths, size_t paths_cap, size_t* paths_len) {
+    if (!ctx || !values || !paths_len) return fail(ctx, FRI_EINVAL, "null argument");
+    const Plan& p = ctx->plan;
+    if (!p.valid || ctx->h_state->n_layers == 0) return fail(ctx, FRI_ESTATE, "no committed layers");
+    if (ctx->sharded_layers)
+        return fail(ctx, FRI_ESTATE, "last commit was sharded: each rank holds only its blocks of the large layers");
+    DecommitPlan dp{};
+    dp.index = index;
+    dp.log_n = p.log_n;
+    dp.n_layers = ctx->h_state->n_layers;
+    uint32_t words = 0;
+    for (uint32_t k = 0; k < dp.n_layers; k++) {
+        dp.layer_off[k] = p.layer_off[k];
+        dp.tree_off[k] = p.tree_off[k];
+        dp.path_off[k] = words;
+        words += 16 * (p.log_n - k);
+    }
+    *paths_len = (size_t)words * 4;
+    if (values_cap < 2 * (size_t)dp.n_layers) return fail(ctx, FRI_EINVAL, "values buffer too small (2 per layer)");
+    if (!paths || paths_cap < (size_t)words * 4) return fail(ctx, FRI_EINVAL, "paths buffer too small (see paths_len)");
+    const size_t total = (2 * (size_t)dp.n_layers + words) * 4;
+    if (!ctx->dq_buf) FRI_HIP(ctx, hipMalloc(&ctx->dq_buf, 65536));
+    if (total > 65536) return fail(ctx, FRI_EINVAL, "decommitment too large");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    launch_decommit_gather(p.layers, p.trees, dp, ctx->dq_buf, ctx->stream);
+    FRI_HIP(ctx, hipGetLastError());
+    std::vector<uint32_t> h(total / 4);
+    FRI_HIP(ctx, hipMemcpyAsync(h.data(), ctx->dq_buf, total, hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    memcpy(values, h.data(), 2 * dp.n_layers * 4);
+    memcpy(paths, h.data() + 2 * dp.n_layers, (size_t)words * 4);
     return FRI_OK;
 }
 

@@ -70,6 +70,15 @@ void launch_coset_points(uint32_t* out, size_t count, uint32_t offset, uint32_t 
 void launch_square_mont(const uint32_t* in, uint32_t* out, size_t count, hipStream_t s);
 void launch_evaluate(const uint32_t* coeffs, size_t d, const uint32_t* xs, size_t count,
                      uint32_t* out, hipStream_t s);
+struct DecommitPlan {
+    uint64_t index;
+    uint32_t log_n, n_layers;
+    uint64_t layer_off[MAXR + 1];
+    uint64_t tree_off[MAXR + 1];
+    uint32_t path_off[MAXR + 1];   // word offset of layer k's two paths (16 * L_j per earlier layer)
+};
+void launch_decommit_gather(const uint32_t* layers, const uint32_t* trees, const DecommitPlan& dp, uint32_t* out,
+                            hipStream_t s);
 void launch_fold_plain(const uint32_t* in, uint32_t* out, uint32_t log_m, const uint32_t* xinv_m,
                        uint32_t beta, hipStream_t s);
 

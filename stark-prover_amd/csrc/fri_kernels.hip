@@ -333,4 +333,37 @@ void launch_fold_plain(const uint32_t* in, uint32_t* out, uint32_t log_m, const 
                        to_mont(beta), (const DevState*)nullptr, 0);
 }
 
+// Decommitment gather for one query (fri_commit.rs:137-163): block k reads
+// layer k's value at idx = index % m_k and at its sibling (idx + m_k/2) % m_k,
+// and the two authentication paths (sibling digest per level, leaf -> root),
+// as raw big-endian bytes.  One launch + one copy per query.
+__global__ void k_decommit_gather(const uint32_t* __restrict__ layers, const uint32_t* __restrict__ trees,
+                                  DecommitPlan dp, uint32_t* __restrict__ out) {
+    const uint32_t k = blockIdx.x;
+    const uint32_t L = dp.log_n - k;
+    const uint64_t m = (uint64_t)1 << L;
+    const uint64_t idx = dp.index % m;
+    const uint64_t sib = (idx + m / 2) % m;
+    if (threadIdx.x == 0) {
+        out[2 * k] = layers[dp.layer_off[k] + idx];
+        out[2 * k + 1] = layers[dp.layer_off[k] + sib];
+    }
+    const uint32_t l = threadIdx.x;
+    if (l >= L) return;
+    const uint32_t* tr = trees + dp.tree_off[k];
+    uint32_t* paths = out + 2 * dp.n_layers + dp.path_off[k];
+#pragma unroll
+    for (int which = 0; which < 2; which++) {
+        const uint64_t leaf = which ? sib : idx;
+        const uint32_t* d = tr + 8 * (level_offset(L, l) + ((leaf >> l) ^ 1u));
+        uint32_t* o = paths + (size_t)which * 8 * L + 8 * l;
+#pragma unroll
+        for (int w = 0; w < 8; w++) o[w] = __builtin_bswap32(d[w]);
+    }
+}
+void launch_decommit_gather(const uint32_t* layers, const uint32_t* trees, const DecommitPlan& dp, uint32_t* out,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_decommit_gather, dim3(dp.n_layers), dim3(64), 0, s, layers, trees, dp, out);
+}
+
 }  // namespace fri

@@ -101,6 +101,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_layer_copy": (i32, [vp, u32, pu32, sz]),
         "fri_tree_level_copy": (i32, [vp, u32, u32, ctypes.c_char_p, sz]),
         "fri_auth_path": (i32, [vp, u32, ctypes.c_uint64, pu32, ctypes.c_char_p, ctypes.POINTER(u32)]),
+        "fri_decommit_query": (i32, [vp, ctypes.c_uint64, pu32, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]),
         "fri_set_profiling": (i32, [vp, i32]),
         "fri_get_profile": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
@@ -242,6 +243,21 @@ class Context:
         dep = ctypes.c_uint32()
         self._check(self.lib.fri_auth_path(self.h, k, index, ctypes.byref(val), buf, ctypes.byref(dep)))
         return val.value, [buf.raw[32 * i: 32 * i + 32] for i in range(dep.value)]
+
+    def decommit_query(self, index: int, n_layers: int, log_n: int):
+        """fri_decommit_query: per committed layer k, (value[idx], value[sib],
+        path(idx), path(sib)) with idx = index % m_k, sib = (idx + m_k/2) % m_k."""
+        vals = np.empty(2 * n_layers, dtype=np.uint32)
+        total = sum(64 * (log_n - k) for k in range(n_layers))
+        buf = ctypes.create_string_buffer(max(total, 1))
+        ln = ctypes.c_size_t()
+        self._check(self.lib.fri_decommit_query(self.h, index, _ptr(vals), vals.size, buf, total, ctypes.byref(ln)))
+        out, off = [], 0
+        for k in range(n_layers):
+            pl = 32 * (log_n - k)
+            out.append((int(vals[2 * k]), int(vals[2 * k + 1]), buf.raw[off:off + pl], buf.raw[off + pl:off + 2 * pl]))
+            off += 2 * pl
+        return out
 
     # ---- multi-GPU ---------------------------------------------------------
     @staticmethod
@@ -414,6 +430,29 @@ class FRIProof:
     @property
     def final_poly(self) -> List[int]:
         return [] if self.final_degree == -1 else [self.final_value]
+
+
+def decommit_fri_layers(index: int, proof: "FRIProof", channel: Channel) -> None:
+    """src/fri/fri_commit.rs:137-163 over the device-resident layers/trees:
+    per layer send value, path, sibling value, sibling path (a 1-element
+    layer first sends its value, as the reference does)."""
+    for val, sval, path, spath in proof.ctx.decommit_query(index, proof.n_layers, proof.log_n):
+        # the gather reads layers of 2^(log_n-k) >= 2 elements; a 1-element
+        # layer (blowup 1) has idx = sib = 0 and empty paths
+        if not path and not spath:
+            channel.send(val.to_bytes(8, "big"))
+        channel.send(val.to_bytes(8, "big"))
+        channel.send(path)
+        channel.send(sval.to_bytes(8, "big"))
+        channel.send(spath)
+
+
+def decommit_fri(num_queries: int, max_index: int, proof: "FRIProof", channel: Channel) -> None:
+    """src/fri/fri_commit.rs:168-179: each index drawn with
+    receive_random_int(0, max_index, true) from the transcript so far."""
+    for _ in range(num_queries):
+        idx = channel.receive_random_int(0, max_index, True)
+        decommit_fri_layers(idx, proof, channel)
 
 
 _CTX_CACHE = {}

@@ -6,8 +6,10 @@
 The reference (Rust, nightly, crates not vendored) cannot be built or run in
 this image, so these vectors are this repo's frozen-spec
 restatement, cross-checked against the independent C oracle by
-tests/test_oracle.py.  Layers are stored as SHA-256 of their little-endian
-u32 bytes plus the first 8 values.
+tests/test_oracle_crosscheck.py.  Layers are stored as SHA-256 of their little-endian
+u32 bytes plus the first 8 values.  "decommit_q3" continues each case's
+channel with decommit_fri(3, n - 1, ...) (fri_commit.rs:137-179): the state
+after it, and the SHA-256 of the proof messages it appended.
 """
 import hashlib
 import json
@@ -26,6 +28,11 @@ def layer_digest(vals):
 def case(name, coeffs, log_n, state="", forced=None, offset=fo.GEN):
     ch = fo.Channel(state=state)
     r = fo.fri_commit(coeffs, log_n, ch, offset=offset, forced_betas=forced)
+    commit_state, commit_proof_size, n_msgs = ch.state, ch.proof_size(), len(ch.proof)
+    fo.decommit_fri(3, (1 << log_n) - 1, r.layers, r.trees, ch)
+    decommit = {"state": ch.state, "messages": len(ch.proof) - n_msgs,
+                "proof_sha256": hashlib.sha256(b"".join(len(m).to_bytes(4, "little") + m
+                                                        for m in ch.proof[n_msgs:])).hexdigest()}
     return {
         "name": name,
         "log_n": log_n,
@@ -37,8 +44,9 @@ def case(name, coeffs, log_n, state="", forced=None, offset=fo.GEN):
         "betas": r.betas,
         "final_value": r.final_value,
         "final_degree": r.final_degree,
-        "channel_out": ch.state,
-        "proof_size": ch.proof_size(),
+        "channel_out": commit_state,
+        "proof_size": commit_proof_size,
+        "decommit_q3": decommit,
         "layer_sha256": [layer_digest(l) for l in r.layers],
         "layer_head": [[int(v) for v in l[:8]] for l in r.layers],
         "leaf0_head": [h.hex() for h in r.trees[0][0][:4]],

@@ -273,3 +273,57 @@ def test_error_codes(ctx):
     assert e.value.code == fri_amd.FRI_EINVAL
     with pytest.raises(fri_amd.FriError):
         ctx.lde([1, 2], 30)                                  # beyond context capacity
+
+
+# ---- decommitment: fri_decommit_query + host mirror (fri_commit.rs:137-179) --
+def _proof_hash(msgs):
+    import hashlib
+    return hashlib.sha256(b"".join(len(m).to_bytes(4, "little") + m for m in msgs)).hexdigest()
+
+
+def test_decommit_matches_golden(ctx, golden):
+    import fri_amd
+    for c in golden["cases"]:
+        if c["forced_betas"] is not None:
+            continue                      # the reference surface has no forced betas
+        ch = fri_amd.Channel(state=c["channel_in"])
+        proof = fri_amd.fri_commit(c["coeffs"], c["log_n"], ch, offset=c["offset"], ctx=ctx)
+        assert ch.state == c["channel_out"], c["name"]
+        n0 = len(ch.proof)
+        fri_amd.decommit_fri(3, (1 << c["log_n"]) - 1, proof, ch)
+        want = c["decommit_q3"]
+        assert ch.state == want["state"], c["name"]
+        assert len(ch.proof) - n0 == want["messages"], c["name"]
+        assert _proof_hash(ch.proof[n0:]) == want["proof_sha256"], c["name"]
+
+
+@pytest.mark.parametrize("log_n,seed,queries", [(16, 5, 8), (20, 6, 4)])
+def test_decommit_matches_oracle_large(ctx, oracle, log_n, seed, queries):
+    """Device gather at scale vs the oracle's rs_merkle proofs, over the same
+    (bit-exact, separately tested) layers."""
+    import fri_amd
+    coeffs = oracle.splitmix64_field(seed, (1 << log_n) // 8)
+    ch = fri_amd.Channel()
+    proof = fri_amd.fri_commit(coeffs, log_n, ch, ctx=ctx)
+    layers = [[int(v) for v in proof.layer(k)] for k in range(proof.n_layers)]
+    trees = [oracle.merkle_levels(l) for l in layers]
+    assert [t[-1][0] for t in trees] == proof.roots
+    och = oracle.Channel(state=ch.state)
+    n0 = len(ch.proof)
+    fri_amd.decommit_fri(queries, (1 << log_n) - 1, proof, ch)
+    oracle.decommit_fri(queries, (1 << log_n) - 1, layers, trees, och)
+    assert ch.state == och.state
+    assert ch.proof[n0:] == och.proof
+
+
+def test_decommit_errors(ctx):
+    import ctypes
+
+    import fri_amd
+    vals = np.zeros(64, dtype=np.uint32)
+    ln = ctypes.c_size_t()
+    fri_amd.fri_commit(list(range(1, 17)), 7, fri_amd.Channel(), ctx=ctx)
+    rc = ctx.lib.fri_decommit_query(ctx.h, 3, vals.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 64, None, 0,
+                                    ctypes.byref(ln))
+    assert rc == fri_amd.FRI_EINVAL                            # no paths buffer ...
+    assert ln.value == sum(64 * (7 - k) for k in range(5))     # ... but the size is reported (5 layers)

@@ -187,3 +187,43 @@ def test_degree_bookkeeping_beta_zero(oracle):
 def test_commit_rejects_domain_exhaustion(oracle):
     with pytest.raises(ValueError):
         oracle.fri_commit([1] * 9, 3, oracle.Channel())
+
+
+# ---- decommitment (fri_commit.rs:137-179) ---------------------------------
+def _verify_path(leaf_value, idx, path, n, root):
+    """Recompute the root from a leaf and its rs_merkle single-leaf proof."""
+    import hashlib
+    h = hashlib.sha256(int(leaf_value).to_bytes(8, "big")).digest()
+    width, off = n, 0
+    while width > 1:
+        sib = idx ^ 1
+        if sib < width:
+            s = path[off:off + 32]
+            off += 32
+            h = hashlib.sha256(s + h if idx & 1 else h + s).digest()
+        idx >>= 1
+        width = (width + 1) // 2
+    assert off == len(path)
+    return h == root
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 13, 64, 100])
+def test_merkle_proof_verifies(oracle, n):
+    vals = oracle.splitmix64_field(n, n)
+    levels = oracle.merkle_levels(vals)
+    for idx in range(n):
+        assert _verify_path(vals[idx], idx, oracle.merkle_proof(levels, idx), n, levels[-1][0])
+
+
+def test_golden_decommit_reproduces(oracle, golden):
+    import hashlib
+    for c in golden["cases"]:
+        ch = oracle.Channel(state=c["channel_in"])
+        r = oracle.fri_commit(c["coeffs"], c["log_n"], ch, offset=c["offset"], forced_betas=c["forced_betas"])
+        n0 = len(ch.proof)
+        oracle.decommit_fri(3, (1 << c["log_n"]) - 1, r.layers, r.trees, ch)
+        want = c["decommit_q3"]
+        assert ch.state == want["state"], c["name"]
+        assert len(ch.proof) - n0 == want["messages"]
+        got = hashlib.sha256(b"".join(len(m).to_bytes(4, "little") + m for m in ch.proof[n0:])).hexdigest()
+        assert got == want["proof_sha256"], c["name"]
