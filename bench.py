@@ -130,6 +130,7 @@ def main():
                 ctx.attach_torch(rank, world)
             else:
                 ctx.attach_rccl(rank, world, bytes(uid.numpy()))
+            ctx.dist_selftest(4096)                           # transport sanity before the data path
             res0 = ctx.commit_sharded(coeffs, log_n)
             # check the sharded transcript against this rank's own 1-GPU commit of the same codeword
             ok = int(_same(res0, ctx.commit(coeffs, log_n)))

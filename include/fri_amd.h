@@ -194,6 +194,11 @@ int fri_dist_attach_rccl(fri_ctx* ctx, int rank, int world, const uint8_t uid[12
 /* Host-callback transport (e.g. torch.distributed gloo; used by tests). */
 int fri_dist_attach_host(fri_ctx* ctx, int rank, int world, const fri_collectives* ops);
 int fri_dist_detach(fri_ctx* ctx);
+/* Diagnostic: run the transport's all-to-all, all-gather and pair exchange
+ * (both streams) on a known pattern and check the result; FRI_ERCCL with a
+ * message on mismatch.  Collective: every rank must call it.  world == 1
+ * exercises the same calls as self-communication. */
+int fri_dist_selftest(fri_ctx* ctx, size_t words_per_peer);
 
 /* Sharded fri_commit: every rank passes the same full coefficient vector and
  * channel state and gets the same result.  world == 1 is fri_commit.

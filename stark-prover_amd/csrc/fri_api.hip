@@ -878,6 +878,52 @@ extern "C" int fri_dist_detach(fri_ctx* ctx) {
     return FRI_OK;
 }
 
+static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords);
+
+// Transport self-test: all-to-all, all-gather and a pair exchange on both
+// streams/communicators, checked on the host.  Rank r sends word
+// (r << 24) | (p << 16) | i to peer p; the exchange partner is r ^ 1 (itself
+// when world == 1).
+extern "C" int fri_dist_selftest(fri_ctx* ctx, size_t words_per_peer) {
+    if (!ctx) return FRI_EINVAL;
+    if (ctx->tp.world < 1 || (!ctx->tp.host && !ctx->tp.comm)) return fail(ctx, FRI_ESTATE, "no transport attached");
+    const uint32_t G = (uint32_t)ctx->tp.world, r = (uint32_t)ctx->tp.rank;
+    if (words_per_peer == 0 || words_per_peer > ((size_t)1 << 16)) return fail(ctx, FRI_EINVAL, "1 <= words_per_peer <= 65536");
+    const size_t W = words_per_peer, tot = W * G;
+    int rc = dist_buffers(ctx, tot, G, tot);
+    if (rc) return rc;
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    std::vector<uint32_t> h(tot), got(tot);
+    for (uint32_t p = 0; p < G; p++)
+        for (size_t i = 0; i < W; i++) h[p * W + i] = (r << 24) | (p << 16) | (uint32_t)i;
+    hipStream_t s = ctx->stream;
+    DistBuf& db = ctx->db;
+    auto check = [&](const char* what, auto expect) -> int {
+        FRI_HIP(ctx, hipMemcpyAsync(got.data(), db.recv, tot * 4, hipMemcpyDeviceToHost, s));
+        FRI_HIP(ctx, hipStreamSynchronize(s));
+        for (uint32_t p = 0; p < G; p++)
+            for (size_t i = 0; i < W; i++)
+                if (got[p * W + i] != expect(p, (uint32_t)i))
+                    return fail(ctx, FRI_ERCCL, std::string("selftest ") + what + " mismatch");
+        return FRI_OK;
+    };
+    FRI_HIP(ctx, hipMemcpyAsync(db.cyc, h.data(), tot * 4, hipMemcpyHostToDevice, s));
+    if ((rc = tp_alltoall(ctx, db.cyc, db.recv, W * 4, s))) return rc;
+    if ((rc = check("alltoall", [&](uint32_t p, uint32_t i) { return (p << 24) | (r << 16) | i; }))) return rc;
+    if ((rc = tp_allgather(ctx, db.cyc, db.recv, W * 4, s))) return rc;      // each rank's first W words
+    if ((rc = check("allgather", [&](uint32_t p, uint32_t i) { return (p << 24) | i; }))) return rc;
+    const uint32_t partner = G > 1 ? (r ^ 1u) : r;
+    // pair exchange on the exchange stream / split communicator, as the fold uses it
+    FRI_HIP(ctx, hipEventRecord(ctx->ev_vals, s));
+    FRI_HIP(ctx, hipStreamWaitEvent(ctx->xstream, ctx->ev_vals, 0));
+    if ((rc = tp_sendrecv(ctx, db.cyc, db.recv, tot * 4, (int)partner, ctx->tp.host ? s : ctx->xstream))) return rc;
+    FRI_HIP(ctx, hipEventRecord(ctx->ev_xchg, ctx->tp.host ? s : ctx->xstream));
+    FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_xchg, 0));
+    if ((rc = check("sendrecv", [&](uint32_t p, uint32_t i) { return (partner << 24) | (p << 16) | i; }))) return rc;
+    ctx->err.clear();
+    return FRI_OK;
+}
+
 static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
     DistBuf& b = ctx->db;
     const size_t nhi = 1u << 20;   // pow table hi part, generous (M <= 2^32)

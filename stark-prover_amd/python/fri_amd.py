@@ -111,6 +111,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_dist_attach_rccl": (i32, [vp, i32, i32, ctypes.c_char_p]),
         "fri_dist_attach_host": (i32, [vp, i32, i32, ctypes.POINTER(Collectives)]),
         "fri_dist_detach": (i32, [vp]),
+        "fri_dist_selftest": (i32, [vp, sz]),
         "fri_commit_sharded": (i32, [vp, pu32, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
                                      ctypes.POINTER(CommitResult)]),
         "fri_commit_sharded_device": (i32, [vp, vp, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
@@ -321,6 +322,9 @@ class Context:
 
     def detach(self):
         self._check(self.lib.fri_dist_detach(self.h))
+
+    def dist_selftest(self, words_per_peer: int = 4096):
+        self._check(self.lib.fri_dist_selftest(self.h, words_per_peer))
 
     def commit_sharded(self, coeffs, log_n: int, offset: int = GENERATOR, channel_state: Optional[bytes] = None,
                        forced_betas: Optional[Sequence[int]] = None) -> CommitResult:

@@ -37,6 +37,7 @@ def main():
         import fri_amd
         ctx = fri_amd.Context(0, log_n)
         ctx.attach_torch(rank, world)
+        ctx.dist_selftest(1024)
         r = ctx.commit_sharded(coeffs, log_n)
         res = {"roots": [bytes(r.roots[k]).hex() for k in range(r.n_layers)],
                "betas": [int(r.betas[i]) for i in range(r.n_rounds)],

@@ -78,3 +78,18 @@ def test_sharded_commit_gpu_matches_single(world, corc, oracle):
         assert r["state"] == och.state.decode()
         assert r["layer0_refused"] and r["tail_matches_single"] and r["auth_matches_single"]
         assert r["single_root0"] == want_roots[0]
+
+
+@pytest.mark.gpu
+def test_rccl_transport_selftest_world1():
+    """The RCCL data path's calls (grouped send/recv all-to-all, all-gather,
+    pair exchange on the split communicator + exchange stream) on the real
+    device, as self-communication: multi-rank RCCL needs one GPU per rank."""
+    import fri_amd
+    ctx = fri_amd.Context(0, 12)
+    try:
+        ctx.attach_rccl(0, 1, fri_amd.Context.unique_id())
+        ctx.dist_selftest(4096)
+        ctx.detach()
+    finally:
+        ctx.close()
