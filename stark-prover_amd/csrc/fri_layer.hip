@@ -282,6 +282,28 @@ __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L
     }
 }
 
+// One scalar load per 64-byte line of every __constant__ table the compact
+// SHA forms read (KTAB, PAD_KW_C, PAD_KW_1024, PAD_KW_1536, 256 B each):
+// fills the CU's scalar cache while the inputs load, instead of cold misses
+// inside level 1 and inside the channel send.  Loads land in clobbered SGPRs
+// and are drained inside the statement.
+__device__ __forceinline__ void ktouch(const void* sym) {
+    uint32_t a, b, c, d;
+    asm volatile("s_nop 4\n\t"
+                 "s_load_dword %0, %4, 0x0\n\ts_load_dword %1, %4, 0x40\n\t"
+                 "s_load_dword %2, %4, 0x80\n\ts_load_dword %3, %4, 0xc0\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b), "=&s"(c), "=&s"(d)
+                 : "s"(sym)
+                 : "memory");
+}
+__device__ __forceinline__ void kcache_touch_sha_tables() {
+    ktouch(&shaf::KTAB[0]);
+    ktouch(&shaf::PAD_KW_C.kw[0]);
+    ktouch(&shaf::PAD_KW_1024.kw[0]);
+    ktouch(&shaf::PAD_KW_1536.kw[0]);
+}
+
 // ------------------------------------------------------------ channel ----
 // Frozen spec: messages are built word by word in registers.
 __device__ __forceinline__ uint32_t hexch(uint32_t nib) { return nib < 10u ? 0x30u + nib : 0x57u + nib; }
@@ -401,6 +423,10 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     const bool pre_wave = COMMIT && threadIdx.x >= 448;
     ChanPre cp;
     if (pre_wave) chanpre_init(cp, t.st);
+    // wave 6 pulls the compact-SHA constant tables into the scalar cache
+    // while the inputs load (they are otherwise cold misses inside level 1
+    // and inside the channel send)
+    if (threadIdx.x >= 384 && threadIdx.x < 448) kcache_touch_sha_tables();
     uint4* A = lds;
     uint4* B = lds + 2 * 1024;
     uint32_t* tr = t.tree;
@@ -445,7 +471,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
             dg_lds_store(B + 2 * q, o);
             dg_store(out + 8 * q, o);
         }
-        if (pre_wave && cnt <= 448 && cp.step < 3) chanpre_step(cp);
+        if (pre_wave && cnt <= 192 && cp.step < 3) chanpre_step(cp);   // SIMD 3 idle from here
         lds_barrier();
         uint4* tmp = A; A = B; B = tmp;
         if (lv - l < 12) TOP_STAMP(1 + lv - l);

@@ -64,8 +64,10 @@ struct PadKW {
 };
 constexpr PadKW PAD_KW{};
 // Padding-only final blocks of 128- and 192-byte messages (channel sends).
-__constant__ constexpr PadKW PAD_KW_1024{1024u};
-__constant__ constexpr PadKW PAD_KW_1536{1536u};
+// (plain __constant__, not constexpr: one symbol per table, read by scalar
+// loads, so a scalar-cache touch at kernel start covers every later use)
+__constant__ PadKW PAD_KW_1024{1024u};
+__constant__ PadKW PAD_KW_1536{1536u};
 
 // Rounds on a register-resident schedule w[16] (consumed).  Variables are
 // rotated by renaming through the 8-way unrolled macro.
@@ -119,7 +121,7 @@ __device__ __forceinline__ void rounds_kwtab(uint32_t st[8], const uint32_t* kw)
 // ---- compact forms for latency-bound code (executed once per launch, so
 // I-cache footprint matters more than the last few percent of issue rate):
 // 16 rounds unrolled, looped 4x; K and padding schedules via scalar loads.
-__constant__ constexpr uint32_t KTAB[64] = {
+__constant__ uint32_t KTAB[64] = {
     0x428a2f98u,0x71374491u,0xb5c0fbcfu,0xe9b5dba5u,0x3956c25bu,0x59f111f1u,0x923f82a4u,0xab1c5ed5u,
     0xd807aa98u,0x12835b01u,0x243185beu,0x550c7dc3u,0x72be5d74u,0x80deb1feu,0x9bdc06a7u,0xc19bf174u,
     0xe49b69c1u,0xefbe4786u,0x0fc19dc6u,0x240ca1ccu,0x2de92c6fu,0x4a7484aau,0x5cb0a9dcu,0x76f988dau,
@@ -128,7 +130,7 @@ __constant__ constexpr uint32_t KTAB[64] = {
     0xa2bfe8a1u,0xa81a664bu,0xc24b8b70u,0xc76c51a3u,0xd192e819u,0xd6990624u,0xf40e3585u,0x106aa070u,
     0x19a4c116u,0x1e376c08u,0x2748774cu,0x34b0bcb5u,0x391c0cb3u,0x4ed8aa4au,0x5b9cca4fu,0x682e6ff3u,
     0x748f82eeu,0x78a5636fu,0x84c87814u,0x8cc70208u,0x90befffau,0xa4506cebu,0xbef9a3f7u,0xc67178f2u};
-__constant__ constexpr PadKW PAD_KW_C{};
+__constant__ PadKW PAD_KW_C{};
 
 #define SHAF_R(kwv)                                                            \
     {                                                                          \
