@@ -33,8 +33,13 @@ constexpr uint32_t INV2_M2 = 0x80000000u;   // Montgomery(2^-1) = 2^31 mod p
     do {                                                                                 \
         if (COMMIT && threadIdx.x == 0) t.st->stamps[t.k][(i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+#define TOP_STAMP_T(i, tid_)                                                                       \
+    do {                                                                                           \
+        if (COMMIT && threadIdx.x == (tid_)) t.st->stamps[t.k][(i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 #else
 #define TOP_STAMP(i) do {} while (0)
+#define TOP_STAMP_T(i, tid_) do {} while (0)
 #endif
 
 __device__ __forceinline__ uint32_t fold1(uint32_t a, uint32_t b, uint32_t xinv_m, uint32_t beta_m) {
@@ -321,60 +326,52 @@ __device__ __forceinline__ uint32_t hexhex(uint32_t b) {
     return 0x33303330u + x + ge * 0x2F7u;
 }
 
-// Channel prework (off the critical path, done by an idle wave during the
-// narrow tree levels): the deferred rehash of the previous receive
-// (channel.rs:75-76, state = sha256_hex(state)) and the midstate of the next
-// send's first block hex(state) (channel.rs:36-39).  Three steps, one
-// compression each; steps that do not apply are skipped.
-struct ChanPre {
-    uint32_t st[8];      // true current state (after the deferred rehash)
-    uint32_t mid[8];     // compress(IV, hex(st))
-    int step;            // next step: 0 rehash block, 1 rehash pad, 2 midstate, 3 done
-};
-__device__ __forceinline__ void chanpre_init(ChanPre& c, const DevState* st) {
-    #pragma unroll
-    for (int i = 0; i < 8; i++) c.st[i] = st->chan[i];
-    c.step = !st->chan_has ? 3 : (st->chan_pending ? 0 : 2);
-}
-__device__ __forceinline__ void chanpre_step(ChanPre& c) {  // compact forms: off the critical path
-    uint32_t w[16];
-    if (c.step == 0) {
-        #pragma unroll
-        for (int i = 0; i < 8; i++) hex2(c.st[i], w[2 * i], w[2 * i + 1]);
-        sha::init(c.mid);
-        shaf::compress_loop(c.mid, w);            // mid used as scratch for the rehash
-    } else if (c.step == 1) {
-        shaf::kwtab_loop(c.mid, shaf::PAD_KW_C.kw);
-        #pragma unroll
-        for (int i = 0; i < 8; i++) c.st[i] = c.mid[i];
-    } else if (c.step == 2) {
-        #pragma unroll
-        for (int i = 0; i < 8; i++) hex2(c.st[i], w[2 * i], w[2 * i + 1]);
-        sha::init(c.mid);
-        shaf::compress_loop(c.mid, w);
-    }
-    c.step++;
-}
+// Channel work of one top kernel as a sequence of compression jobs run by
+// wave 7 (lanes redundant), with ONE compress_loop and ONE kwtab_loop call
+// site: the jobs done during the narrow tree levels (off the critical path)
+// leave exactly the code the post-root jobs need in the I-cache.
+//   0  rehash block   X = compress(IV, hex(cs))        channel.rs:75-76, the
+//   1  rehash pad     cs = X = pad(X)                  receive's deferred rehash
+//   2  midstate       X = compress(IV, hex(cs))        first block of the next send
+//   3  root block 1   X = compress(X | IV, hex(hex(root[0..15])))   channel.rs:35-39,
+//   4  root block 2   X = compress(X, hex(hex(root[16..31])))       message = root hex
+//   5  root pad       cs = X = pad_{1536|1024}(X)      -> S
+//   6  final block 1  X = compress(IV, hex(cs))        fri_commit.rs:114,
+//   7  final block 2  cs = X = compress(X, hex(be64(fv)) | pad)   send(final.to_bytes())
+enum { CJ_REHASH = 0, CJ_MID = 2, CJ_ROOT = 3, CJ_FINAL = 6, CJ_END_ROUND = 6, CJ_END_FINAL = 8 };
 
-// channel.rs:35-44 with message = root_hex bytes (frozen spec):
-// state = sha256_hex(state || hex(root_hex)).  `mid` = compress(IV, hex(state))
-// when has_state; the two hex(hex(root)) blocks and the constant padding
-// block remain (3 compressions).
-__device__ __forceinline__ void chan_send_root(uint32_t has, const uint32_t mid[8], const uint32_t root[8],
-                                               uint32_t out[8]) {
+__device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[8], uint32_t has, const uint4* root_lds,
+                                         uint32_t fv) {
     uint32_t w[16];
-    if (has) { for (int i = 0; i < 8; i++) out[i] = mid[i]; }
-    else sha::init(out);
-    #pragma unroll
-    for (int blk = 0; blk < 2; blk++) {
-        #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int byte = blk * 16 + j;
-            w[j] = hexhex((root[byte >> 2] >> (24 - 8 * (byte & 3))) & 255u);
+    const bool pad = (j == 1) || (j == 5);
+    if (j == 0 || j == 2 || j == 6) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) hex2(cs[i], w[2 * i], w[2 * i + 1]);
+        sha::init(X);
+    } else if (j == 3 || j == 4) {
+        Dg r;
+        dg_lds_load(root_lds, r);
+        const bool hi = (j == 4);
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) {
+            const uint32_t rw = hi ? r.w[4 + (jj >> 2)] : r.w[jj >> 2];
+            w[jj] = hexhex((rw >> (24 - 8 * (jj & 3))) & 255u);
         }
-        shaf::compress_loop(out, w);
+        if (j == 3 && !has) sha::init(X);
+    } else if (j == 7) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = 0u;
+        w[0] = 0x30303030u; w[1] = 0x30303030u;   // "00000000": high u32 of the u64 is 0
+        hex2(fv, w[2], w[3]);
+        w[4] = 0x80000000u;
+        w[15] = 80u * 8u;                           // hex(state) (64) + 16 chars
     }
-    shaf::kwtab_loop(out, has ? shaf::PAD_KW_1536.kw : shaf::PAD_KW_1024.kw);
+    if (pad) shaf::kwtab_loop(X, j == 1 ? shaf::PAD_KW_C.kw : (has ? shaf::PAD_KW_1536.kw : shaf::PAD_KW_1024.kw));
+    else shaf::compress_loop(X, w);
+    if (j == 1 || j == 5 || j == 7) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) cs[i] = X[i];
+    }
 }
 
 // channel.rs:47-72: beta = U256(state) mod p  (the rehash is deferred)
@@ -389,52 +386,44 @@ __device__ __forceinline__ uint32_t chan_beta(const uint32_t s[8]) {
     return r;
 }
 
-// fri_commit.rs:114: send(final.to_bytes()) — state || 16 hex chars of the
-// 8-byte big-endian value.  `s` is the state right after the last root send
-// (no receive in between, so no rehash).
-__device__ __forceinline__ void chan_send_final(const uint32_t s[8], uint32_t fv, uint32_t out[8]) {
-    uint32_t w[16];
-    sha::init(out);
-    #pragma unroll
-    for (int i = 0; i < 8; i++) hex2(s[i], w[2 * i], w[2 * i + 1]);
-    shaf::compress_loop(out, w);
-    #pragma unroll
-    for (int j = 0; j < 16; j++) w[j] = 0u;
-    w[0] = 0x30303030u; w[1] = 0x30303030u;          // "00000000": high u32 of the u64 is 0
-    hex2(fv, w[2], w[3]);
-    w[4] = 0x80000000u;
-    w[15] = 80u * 8u;
-    shaf::compress_loop(out, w);
-}
-
 // ---------------------------------------------------------------- top ----
 // One workgroup.  FROM_LEAVES: the layer has N = 2^L <= 1024 elements and is
 // done entirely here (fold, leaves, all levels, whole coefficient task).
 // Otherwise: N = 2^(L-l) <= 1024 level-l digests -> root.
+// COMMIT: the degree of poly_k is reduced up front (its inputs are complete
+// at launch); wave 7 runs the channel jobs (chan_job) during the levels whose
+// nodes fit waves 0-2, then after the root, in extra iterations of the level
+// loop (uniform barrier count).
 template <bool FROM_LEAVES, bool FOLD, bool COMMIT>
 __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const int32_t* mx, uint32_t G) {
     if (gated_off(t)) return;
     __shared__ uint4 lds[2 * 1024 + 2 * 512];
     __shared__ int32_t red[24];
-    __shared__ uint32_t pre_sh[16];
     const uint32_t L = t.L;
     const uint32_t N = 1u << (L - l);
-    // wave 7 carries the channel prework through the narrow levels
-    const bool pre_wave = COMMIT && threadIdx.x >= 448;
-    ChanPre cp;
-    if (pre_wave) chanpre_init(cp, t.st);
+    const uint32_t tid = threadIdx.x;
+    const bool chan_wave = COMMIT && tid >= 448;
+    DevState* st = t.st;
+    uint32_t cs[8], X[8];
+    uint32_t has = 0;
+    int job = CJ_END_FINAL;
+    if (chan_wave) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) cs[i] = st->chan[i];
+        has = st->chan_has;
+        job = !has ? CJ_ROOT : (st->chan_pending ? CJ_REHASH : CJ_MID);
+    }
     // wave 6 pulls the compact-SHA constant tables into the scalar cache
-    // while the inputs load (they are otherwise cold misses inside level 1
-    // and inside the channel send)
-    if (threadIdx.x >= 384 && threadIdx.x < 448) kcache_touch_sha_tables();
+    // while the inputs load (cold misses inside level 1 and the channel otherwise)
+    if (tid >= 384 && tid < 448) kcache_touch_sha_tables();
     uint4* A = lds;
     uint4* B = lds + 2 * 1024;
     uint32_t* tr = t.tree;
     TOP_STAMP(0);
     if (FROM_LEAVES) {
         const size_t half = (size_t)1 << L;
-        const uint32_t beta_m = FOLD ? (COMMIT ? t.st->beta_mont[t.k - 1] : t.beta_m) : 0u;
-        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+        const uint32_t beta_m = FOLD ? (COMMIT ? st->beta_mont[t.k - 1] : t.beta_m) : 0u;
+        for (uint32_t i = tid; i < N; i += blockDim.x) {
             uint32_t v;
             if (FOLD) {
                 v = fold1(t.prev[i], t.prev[i + half], t.xinv[i], beta_m);
@@ -447,70 +436,88 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
             dg_store(tr + 8 * i, d);
             dg_lds_store(A + 2 * i, d);
         }
-        if (COMMIT) { coef_task(t, 0, 1, red); mx = t.wgmax; G = 1; }
+        if (COMMIT) coef_task(t, 0, 1, red);       // per-wave maxima in red[], wgmax[0..2]
     } else {
         const uint32_t* in = tr + 8 * level_offset(L, l);
-        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+        for (uint32_t i = tid; i < N; i += blockDim.x) {
             Dg d;
             dg_load(in + 8 * i, d);
             dg_lds_store(A + 2 * i, d);
         }
-    }
-    __syncthreads();
-    TOP_STAMP(1);
-    uint32_t cnt = N;
-    for (uint32_t lv = l + 1; lv <= L; lv++) {
-        cnt >>= 1;
-        uint32_t* out = tr + 8 * level_offset(L, lv);
-#pragma unroll 1
-        for (uint32_t q = threadIdx.x; q < cnt; q += blockDim.x) {
-            Dg a, b, o;
-            dg_lds_load(A + 4 * q, a);
-            dg_lds_load(A + 4 * q + 2, b);
-            cnode(a, b, o);
-            dg_lds_store(B + 2 * q, o);
-            dg_store(out + 8 * q, o);
+        if (COMMIT) {                              // producer maxima -> per-wave triples
+            int m0 = -1, m1 = -1, m2 = -1;
+            for (uint32_t i = tid; i < G; i += blockDim.x) {
+                m0 = max(m0, mx[3 * i]); m1 = max(m1, mx[3 * i + 1]); m2 = max(m2, mx[3 * i + 2]);
+            }
+            m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
+            if ((tid & 63) == 0) { red[3 * (tid >> 6)] = m0; red[3 * (tid >> 6) + 1] = m1; red[3 * (tid >> 6) + 2] = m2; }
         }
-        if (pre_wave && cnt <= 192 && cp.step < 3) chanpre_step(cp);   // SIMD 3 idle from here
-        lds_barrier();
-        uint4* tmp = A; A = B; B = tmp;
-        if (lv - l < 12) TOP_STAMP(1 + lv - l);
     }
-    if (!COMMIT) return;
-    if (pre_wave) {
-        while (cp.step < 3) chanpre_step(cp);     // short trees: finish here
-        if (threadIdx.x == 448)
+    __syncthreads();
+    // ---- degree of poly_k (reference degree field; see DevState), uniform ----
+    int deg = -1;
+    if (COMMIT) {
+        int m0 = -1, m1 = -1, m2 = -1;
 #pragma unroll
-            for (int i = 0; i < 8; i++) { pre_sh[i] = cp.st[i]; pre_sh[8 + i] = cp.mid[i]; }
+        for (int i = 0; i < 8; i++) { m0 = max(m0, red[3 * i]); m1 = max(m1, red[3 * i + 1]); m2 = max(m2, red[3 * i + 2]); }
+        deg = (t.k == 0) ? m0 : (m1 < 0 ? m2 : m0);
     }
-    // ---- degree of poly_k (reference degree field; see DevState) --------
-    DevState* st = t.st;
-    int m0 = -1, m1 = -1, m2 = -1;
-    for (uint32_t i = threadIdx.x; i < G; i += blockDim.x) {
-        m0 = max(m0, mx[3 * i]); m1 = max(m1, mx[3 * i + 1]); m2 = max(m2, mx[3 * i + 2]);
+    const bool is_final = COMMIT && deg < 1;
+    const int job_end = is_final ? CJ_END_FINAL : CJ_END_ROUND;
+    uint32_t fv = 0;                               // fri_commit.rs:109-113
+    if (chan_wave && is_final && deg == 0) fv = (t.k == 0 ? t.coef_in : t.coef_out)[0];
+    TOP_STAMP(1);
+    // iterations: the levels, then the channel jobs still left after them
+    const uint32_t nlev = L - l;
+    uint32_t total = nlev;
+    if (COMMIT) {
+        const uint32_t n_pre = !st->chan_has ? 0u : (st->chan_pending ? 3u : 1u);
+        const uint32_t pre_in_levels = min(n_pre, min(nlev, 8u));   // levels with <= 128 nodes
+        total += (n_pre - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
     }
-    m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
-    __syncthreads();
-    const uint32_t wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[3 * wave] = m0; red[3 * wave + 1] = m1; red[3 * wave + 2] = m2; }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    for (uint32_t i = 1; i < blockDim.x / 64; i++) { m0 = max(m0, red[3 * i]); m1 = max(m1, red[3 * i + 1]); m2 = max(m2, red[3 * i + 2]); }
-    TOP_STAMP(14);
+    uint32_t cnt = N;
+#pragma unroll 1
+    for (uint32_t it = 0; it < total; it++) {
+        const bool level = it < nlev;
+        if (level) {
+            cnt >>= 1;
+            uint32_t* out = tr + 8 * level_offset(L, l + 1 + it);
+#pragma unroll 1
+            for (uint32_t q = tid; q < cnt; q += blockDim.x) {
+                Dg a, b, o;
+                dg_lds_load(A + 4 * q, a);
+                dg_lds_load(A + 4 * q + 2, b);
+                cnode(a, b, o);
+                dg_lds_store(B + 2 * q, o);
+                dg_store(out + 8 * q, o);
+            }
+        }
+        // channel job: during the narrow levels (SIMD 3 idle) only the
+        // pre-root jobs, after the last level anything left
+        if (chan_wave && job < job_end && (level ? (cnt <= 192 && job < CJ_ROOT) : true)) {
+            chan_job(job, cs, X, has, A, fv);
+            job++;
+        }
+        lds_barrier();
+        if (level) {
+            uint4* tmp = A; A = B; B = tmp;
+            if (it < 11) TOP_STAMP(2 + it);
+        }
+    }
+    if (!COMMIT || tid != 448) return;
+    // ---- results (wave 7, one lane) ----
     const int k = t.k;
-    const int deg = (k == 0) ? m0 : (m1 < 0 ? m2 : m0);
     st->deg[k] = deg;
     Dg root;
     dg_lds_load(A, root);
+#pragma unroll
     for (int i = 0; i < 8; i++) st->roots[k][i] = root.w[i];
-    const uint32_t has = st->chan_has;
-    uint32_t S[8];
-    chan_send_root(has, pre_sh + 8, root.w, S);     // state after send(root_hex)
-    TOP_STAMP(15);
     st->n_layers = (uint32_t)k + 1;
+    TOP_STAMP_T(15, 448);
     if (deg >= 1 && k < MAXR && L >= 1) {
-        uint32_t beta = chan_beta(S);
-        for (int i = 0; i < 8; i++) st->chan[i] = S[i];
+        uint32_t beta = chan_beta(cs);
+#pragma unroll
+        for (int i = 0; i < 8; i++) st->chan[i] = cs[i];
         st->chan_has = 1;
         st->chan_pending = 1;                        // receive's rehash deferred to the next top
         if (st->forced) beta = st->forced_beta[k];
@@ -518,17 +525,14 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         st->beta_mont[k] = to_mont(beta);
         st->active[k] = 1;
         st->n_rounds = (uint32_t)k + 1;
-        TOP_STAMP(16);
+        TOP_STAMP_T(16, 448);
     } else {
         st->active[k] = 0;
         if (deg >= 1) { st->status = 7u; return; }            // FRI_EDEGREE
-        const uint32_t* ck = (k == 0) ? t.coef_in : t.coef_out;
-        uint32_t fv = (deg == -1) ? 0u : ck[0];
+#pragma unroll
+        for (int i = 0; i < 8; i++) st->chan[i] = cs[i];      // after send(final.to_bytes())
         st->final_value = fv;
         st->final_degree = deg;
-        uint32_t F[8];
-        chan_send_final(S, fv, F);
-        for (int i = 0; i < 8; i++) st->chan[i] = F[i];
         st->chan_has = 1;
         st->chan_pending = 0;
     }
