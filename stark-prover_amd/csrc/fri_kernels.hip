@@ -76,22 +76,36 @@ __global__ __launch_bounds__(256) void k_ntt_pass(const uint32_t* src, size_t d,
     }
     __syncthreads();
     uint32_t r[16];
+    // Twiddles.  Stage s = s0 + t of element (column lo, row q) uses
+    // w_{2^(s+1)}^((q mod 2^t) * 2^s0 + lo) = w_{2^(t+1)}^(q mod 2^t) * w_{2^(s+1)}^lo:
+    // a small-table entry (< 2^NS, cached) times a per-column factor.  All 16
+    // elements of a thread share one column in both phases, so the factors
+    // cost one table load per pass (top stage) and squarings below it
+    // (w_{2^s}^lo = (w_{2^(s+1)}^lo)^2) instead of a load of the 2^s-entry
+    // stage table per butterfly.
+    uint32_t wl[NS];
+    if (!FIRST) {
+        const size_t lo = (col0 + ((tid * 16) >> NS)) & lomask;
+        wl[NS - 1] = tw[((size_t)1 << (s0 + NS - 1)) + lo];
+#pragma unroll
+        for (int t = (int)NS - 2; t >= 0; t--) wl[t] = mmul(wl[t + 1], wl[t + 1]);
+    }
+    auto twid = [&](int t, uint32_t q0) -> uint32_t {
+        const uint32_t w = tw[(1u << t) + (q0 & ((1u << t) - 1))];
+        return FIRST ? w : mmul(w, wl[t]);
+    };
     // ---- phase A: stages 0..A-1 on 16 consecutive elements ----------------
 #pragma unroll
     for (int e = 0; e < 16; e++) r[e] = lds[ntt_laddr(tid * 16 + e)];
     {
         const uint32_t x0 = tid * 16;
-        const uint32_t c = x0 >> NS;
-        const size_t lo = FIRST ? 0 : ((col0 + c) & lomask);
 #pragma unroll
         for (int t = 0; t < A; t++) {
-            const uint32_t s = s0 + t;
 #pragma unroll
             for (int e = 0; e < 16; e++) {
                 if (e & (1 << t)) continue;
                 const uint32_t q0 = (x0 + e) & (P - 1);
-                const size_t j = ((size_t)(q0 & ((1u << t) - 1)) << s0) + lo;
-                const uint32_t w = tw[((size_t)1 << s) + j];
+                const uint32_t w = twid(t, q0);
                 const uint32_t u = r[e], v = mmul(r[e + (1 << t)], w);
                 r[e] = add(u, v);
                 r[e + (1 << t)] = sub(u, v);
@@ -112,16 +126,14 @@ __global__ __launch_bounds__(256) void k_ntt_pass(const uint32_t* src, size_t d,
         }
 #pragma unroll
         for (int t = A; t < (int)NS; t++) {
-            const uint32_t s = s0 + t, tb = t - A;
+            const uint32_t tb = t - A;
 #pragma unroll
             for (int e = 0; e < 16; e++) {
                 if (e & (1 << tb)) continue;
                 const uint32_t G = tid * GPT + (e >> B), m = e & ((1u << B) - 1);
-                const uint32_t c = G >> A, ql = G & ((1u << A) - 1);
+                const uint32_t ql = G & ((1u << A) - 1);
                 const uint32_t q0 = ql + (m << A);
-                const size_t lo = FIRST ? 0 : ((col0 + c) & lomask);
-                const size_t j = ((size_t)(q0 & ((1u << t) - 1)) << s0) + lo;
-                const uint32_t w = tw[((size_t)1 << s) + j];
+                const uint32_t w = twid(t, q0);
                 const uint32_t u = r[e], v = mmul(r[e + (1 << tb)], w);
                 r[e] = add(u, v);
                 r[e + (1 << tb)] = sub(u, v);
