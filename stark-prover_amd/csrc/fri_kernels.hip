@@ -36,40 +36,47 @@ __device__ __forceinline__ uint32_t pow2lvl(const uint32_t* lo, const uint32_t* 
 }
 __device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4); }
 
-template <int A, int B, bool FIRST>
-__global__ __launch_bounds__(256) void k_ntt_pass(const uint32_t* src, size_t d, uint32_t* dst,
+#ifndef NTT_TPB
+#define NTT_TPB 512          // threads per NTT tile (16 elements each; 512: 128-byte row runs)
+#endif
+
+template <int A, int B, bool FIRST, int TPB>
+__global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d, uint32_t* dst,
                                                   uint32_t log_n, uint32_t s0, const uint32_t* __restrict__ tw,
                                                   const uint32_t* __restrict__ pre_lo, const uint32_t* __restrict__ pre_hi,
                                                   const uint32_t* __restrict__ post_lo,
                                                   const uint32_t* __restrict__ post_hi) {
-    constexpr uint32_t NS = A + B, P = 1u << NS, C = 4096u / P;
-    __shared__ uint32_t lds[4096 + 256];
+    // tile: 16 elements per thread; C columns (C consecutive words per row)
+    constexpr uint32_t NS = A + B, P = 1u << NS, TILE = 16u * TPB, C = TILE / P;
+    __shared__ uint32_t lds[TILE + TILE / 16];
     const uint32_t tid = threadIdx.x;
     const size_t ncols = ((size_t)1 << log_n) >> NS;
     const size_t col0 = (size_t)blockIdx.x * C;
     const size_t lomask = ((size_t)1 << s0) - 1;
+    // FIRST (bit-reversed input): tile column c is output column
+    // bitrev(col0 + c) over the log_n - NS column bits, so its row q reads
+    // input bitrev_NS(q) * 2^(log_n-NS) + col0 + c: contiguous across c.
+    const uint32_t cbits = log_n - NS;
     auto gidx = [&](uint32_t c, uint32_t q) -> size_t {
         const size_t col = col0 + c;
-        if (FIRST) return col * P + q;
+        if (FIRST) return (size_t)(cbits ? (__brev((uint32_t)col) >> (32 - cbits)) : 0u) * P + q;
         return ((col >> s0) << (s0 + NS)) + ((size_t)q << s0) + (col & lomask);
     };
-    // ---- load (contiguous runs) -------------------------------------------
+    // ---- load (contiguous runs across the tile's columns) -----------------
 #pragma unroll 4
     for (uint32_t r = 0; r < 16; r++) {
-        const uint32_t y = r * 256 + tid;
-        uint32_t c, q;
-        if (FIRST) { c = y / P; q = y % P; } else { c = y % C; q = y / C; }
+        const uint32_t y = r * TPB + tid;
+        const uint32_t c = y % C, q = y / C;
         uint32_t v = 0;
         if (col0 + c < ncols) {
-            const size_t g = gidx(c, q);
             if (FIRST) {
-                const uint32_t si = log_n ? (__brev((uint32_t)g) >> (32 - log_n)) : 0u;
+                const size_t si = ((size_t)(__brev(q) >> (32 - NS)) << cbits) + col0 + c;
                 if (si < d) {
                     v = src[si];
                     if (pre_lo) v = pow2lvl(pre_lo, pre_hi, si, v);
                 }
             } else {
-                v = src[g];
+                v = src[gidx(c, q)];
             }
         }
         lds[ntt_laddr(c * P + q)] = v;
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(256) void k_ntt_pass(const uint32_t* src, size_t d,
     // ---- store (contiguous runs) ------------------------------------------
 #pragma unroll 4
     for (uint32_t rr = 0; rr < 16; rr++) {
-        const uint32_t y = rr * 256 + tid;
+        const uint32_t y = rr * TPB + tid;
         uint32_t c, q;
         if (FIRST) { c = y / P; q = y % P; } else { c = y % C; q = y / C; }
         if (col0 + c >= ncols) continue;
@@ -179,14 +186,15 @@ template <bool FIRST>
 static void launch_pass(uint32_t ns, const uint32_t* src, size_t d, uint32_t* dst, uint32_t log_n, uint32_t s0,
                         const NttPlan& p, bool last, hipStream_t s) {
     const size_t n = (size_t)1 << log_n;
-    const unsigned blocks = (unsigned)((n + 4095) / 4096);
+    constexpr int TPB = NTT_TPB;
+    const unsigned blocks = (unsigned)((n + 16 * TPB - 1) / (16 * TPB));
     const uint32_t* plo = FIRST ? p.pre_lo : nullptr;
     const uint32_t* phi = FIRST ? p.pre_hi : nullptr;
     const uint32_t* qlo = last ? p.post_lo : nullptr;
     const uint32_t* qhi = last ? p.post_hi : nullptr;
 #define NTT_CASE(NSV, AV, BV)                                                                                   \
     case NSV:                                                                                                   \
-        hipLaunchKernelGGL((k_ntt_pass<AV, BV, FIRST>), dim3(blocks), dim3(256), 0, s, src, d, dst, log_n, s0, p.tw, \
+        hipLaunchKernelGGL((k_ntt_pass<AV, BV, FIRST, TPB>), dim3(blocks), dim3(TPB), 0, s, src, d, dst, log_n, s0, p.tw, \
                            plo, phi, qlo, qhi);                                                                 \
         break;
     switch (ns) {
