@@ -12,7 +12,7 @@ tr = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
 tr.sort(key=lambda r: int(r["Start_Timestamp"]))
 gx = "Grid_Size" if "Grid_Size" in tr[0] else "Grid_Size_X"
 wx = "Workgroup_Size" if "Workgroup_Size" in tr[0] else "Workgroup_Size_X"
-idx = [i for i, r in enumerate(tr) if "k_ntt_pass" in r["Kernel_Name"] and "true>" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(tr) if "k_ntt_pass" in r["Kernel_Name"] and ", true" in r["Kernel_Name"]]
 s = idx[which]
 e = idx[which + 1] if which + 1 < 0 or which + 1 < len(idx) else len(tr)
 t0 = int(tr[s]["Start_Timestamp"])
