@@ -76,6 +76,12 @@ def _same(a, b):
 
 
 def main():
+    # The contract's ONE JSON line goes to the original stdout; everything
+    # else written to fd 1 by native libraries (gloo connection messages, the
+    # RCCL banner) or by Python is redirected to stderr.
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -124,27 +130,50 @@ def main():
             uid = torch.frombuffer(bytearray(fri_amd.Context.unique_id()), dtype=torch.uint8).clone()
         dist.broadcast(uid, 0)
         coeffs = _coeffs(42, d, fri_amd.P)                    # one polynomial for the whole job
-        ok = 1
-        try:
+
+        def agreed(step):
+            """Run one step of the sharded setup; every rank learns whether ALL
+            ranks succeeded before anyone enters the next collective (a rank that
+            failed alone must not leave the others blocked inside RCCL)."""
+            nonlocal note
+            ok = 1
+            try:
+                if step() is False:
+                    ok, note = 0, note or "sharded transcript differed from the 1-GPU commit"
+            except fri_amd.FriError as e:
+                ok, note = 0, f"sharded path failed: {e}"
+            flag = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            return int(flag.item()) == 1
+
+        attached = False
+
+        def attach():
+            nonlocal attached
             if args.transport == "host":
                 ctx.attach_torch(rank, world)
             else:
                 ctx.attach_rccl(rank, world, bytes(uid.numpy()))
-            ctx.dist_selftest(4096)                           # transport sanity before the data path
+            attached = True
+
+        res0 = None
+
+        def first_commit():
+            nonlocal res0
             res0 = ctx.commit_sharded(coeffs, log_n)
-            # check the sharded transcript against this rank's own 1-GPU commit of the same codeword
-            ok = int(_same(res0, ctx.commit(coeffs, log_n)))
-        except fri_amd.FriError as e:
-            ok, note = 0, f"sharded path failed: {e}"
-        flag = torch.tensor([ok], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag.item()) == 0:
-            note = note or "sharded transcript differed from the 1-GPU commit"
+            # the sharded transcript must equal this rank's own 1-GPU commit
+            return _same(res0, ctx.commit(coeffs, log_n))
+
+        ok = (agreed(attach) and agreed(lambda: ctx.dist_selftest(4096))   # transport sanity first
+              and agreed(first_commit))
+        if not ok:
+            note = note or "another rank failed during the sharded setup"
             print(f"[bench] rank {rank}: {note}; falling back to replicas", file=sys.stderr, flush=True)
-            try:
-                ctx.detach()
-            except fri_amd.FriError:
-                pass
+            if attached:
+                try:
+                    ctx.detach()
+                except fri_amd.FriError:
+                    pass
             ctx.close()
             mode = "replicas"
             log_n = args.log_n
@@ -279,7 +308,7 @@ def main():
         }
         if note:
             line["note"] = note
-        print(json.dumps(line), flush=True)
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     if mode == "sharded":
         ctx.detach()
     ctx.close()
