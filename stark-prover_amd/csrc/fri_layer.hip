@@ -550,6 +550,10 @@ static LayerTask with_gate(const LayerTask& in) {
     return t;
 }
 
+#ifndef QUAD_MIN_LOG
+#define QUAD_MIN_LOG 19      // smaller layers: one leaf per lane (A/B: 19 beats 20 and 21)
+#endif
+
 void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
     const LayerTask t = with_gate(tin);
     const uint32_t L = t.L;
@@ -568,7 +572,7 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
         return;
     }
     uint32_t G, out_per_wg;
-    if (L >= 19) {
+    if (L >= QUAD_MIN_LOG) {
         G = 1u << (L - 10);
         out_per_wg = 64;
         if (fold) {
