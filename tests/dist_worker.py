@@ -22,13 +22,14 @@ sys.path.insert(0, HERE)
 
 def main():
     mode, log_n, seed, out_dir = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    blowup_log = int(sys.argv[5]) if len(sys.argv) > 5 else 3
     import torch.distributed as dist
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     import numpy as np
 
     import fri_oracle as fo
-    d = (1 << log_n) // 8
+    d = (1 << log_n) >> blowup_log
     coeffs = fo.splitmix64_field(seed, d)
     if mode == "model":
         import dist_model

@@ -24,14 +24,14 @@ def free_port():
     return p
 
 
-def run_ranks(mode, world, log_n, seed, timeout, env_extra=None):
+def run_ranks(mode, world, log_n, seed, timeout, env_extra=None, blowup_log=3):
     out = tempfile.mkdtemp(prefix=f"fri_{mode}_")
     env = dict(os.environ)
     env["MASTER_ADDR"] = "127.0.0.1"
     env.update(env_extra or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "tests", "dist_worker.py"), mode, str(log_n), str(seed), out]
+           os.path.join(ROOT, "tests", "dist_worker.py"), mode, str(log_n), str(seed), out, str(blowup_log)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
     res = [json.load(open(os.path.join(out, f"rank{i}.json"))) for i in range(world)]
@@ -56,14 +56,18 @@ def test_sharded_protocol_model_gloo(oracle, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_commit_gpu_matches_single(world, corc, oracle):
+@pytest.mark.parametrize("world,log_n,blowup_log", [
+    (2, 22, 3), (4, 22, 3),          # several sharded layers, then local
+    (2, 20, 3), (2, 21, 3),          # switch to local right after layer 0 / 1
+    (2, 21, 1), (4, 22, 0),          # d > n/G: the coset reduction folds several chunks
+])
+def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, corc, oracle):
     import ctypes
 
     import numpy as np
-    log_n, seed = 22, 7
-    got = run_ranks("gpu", world, log_n, seed, timeout=900)
-    d = (1 << log_n) // 8
+    seed = 7
+    got = run_ranks("gpu", world, log_n, seed, timeout=900, blowup_log=blowup_log)
+    d = (1 << log_n) >> blowup_log
     c = np.ascontiguousarray(np.array(oracle.splitmix64_field(seed, d), dtype=np.uint64))
     och = oracle.OrcChannel()
     corc.orc_channel_init(ctypes.byref(och))

@@ -299,6 +299,44 @@ def test_graph_replay_stable(ctx, oracle):
     assert [a.betas[i] for i in range(13)] == [b.betas[i] for i in range(13)]
 
 
+def _oracle_commit(oracle, coeffs, log_n):
+    ch = oracle.Channel()
+    r = oracle.fri_commit(coeffs, log_n, ch, keep=False)
+    return [x.hex() for x in r.roots], r.betas, r.final_value, ch.state
+
+
+def _gpu_commit(ctx, coeffs, log_n):
+    res = ctx.commit(coeffs, log_n)
+    return ([bytes(res.roots[k]).hex() for k in range(res.n_layers)], [res.betas[r] for r in range(res.n_rounds)],
+            res.final_value, bytes(res.channel_out.digest).hex() if res.channel_out.has_state else "")
+
+
+@pytest.mark.parametrize("log_n,d", [(1, 1), (1, 2), (2, 1), (2, 4), (3, 3), (3, 8), (4, 16), (5, 7), (5, 32)])
+def test_tiny_codewords(ctx, oracle, log_n, d):
+    """Smallest domains, including blowup 1 (d = n): the last layer has one element."""
+    coeffs = oracle.splitmix64_field(100 + log_n * 10 + d, d)
+    assert _gpu_commit(ctx, coeffs, log_n) == _oracle_commit(oracle, coeffs, log_n)
+
+
+def test_plan_reuse_across_sizes(ctx, corc, oracle):
+    """One context, commits of changing size: plans are rebuilt and graphs re-captured."""
+    for log_n in (12, 9, 14, 12, 10, 14):
+        coeffs = oracle.splitmix64_field(log_n, (1 << log_n) // 8)
+        if log_n <= 10:
+            want = _oracle_commit(oracle, coeffs, log_n)
+        else:
+            c = np.array(coeffs, dtype=np.uint64)
+            cs, pc = c_u64(c)
+            och = oracle.OrcChannel()
+            corc.orc_channel_init(ctypes.byref(och))
+            ores = oracle.OrcFriResult()
+            assert corc.orc_fri_commit_fast(pc, len(coeffs), log_n, 5, 5, P, ctypes.byref(och), None,
+                                            ctypes.byref(ores), None, None) == 0
+            want = ([bytes(ores.roots[k]).hex() for k in range(ores.n_layers)],
+                    [ores.betas[r] for r in range(ores.n_rounds)], ores.final_value, och.state.decode())
+        assert _gpu_commit(ctx, coeffs, log_n) == want, log_n
+
+
 def test_error_codes(ctx):
     import fri_amd
     with pytest.raises(fri_amd.FriError) as e:
