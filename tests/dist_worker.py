@@ -52,11 +52,12 @@ def main():
             res["layer0_refused"] = True
         last = r.n_layers - 1
         tail = ctx.layer(last, log_n)
-        _, path = ctx.auth_path(last, 1, log_n)
+        qi = min(1, tail.size - 1)            # a 1-element last layer (blowup 1) has only index 0
+        _, path = ctx.auth_path(last, qi, log_n)
         ctx.detach()
         single = ctx.commit(coeffs, log_n)
         res["tail_matches_single"] = bool(np.array_equal(tail, ctx.layer(last, log_n)))
-        res["auth_matches_single"] = path == ctx.auth_path(last, 1, log_n)[1]
+        res["auth_matches_single"] = path == ctx.auth_path(last, qi, log_n)[1]
         res["single_root0"] = bytes(single.roots[0]).hex()
         ctx.close()
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
