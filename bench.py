@@ -278,6 +278,21 @@ def main():
         pcie = {"ms_per_step": round(1000.0 * (time.perf_counter() - t0) / k, 4),
                 "what": f"fri_commit from a pageable host buffer of {d} u32 coefficients (H2D inside the call)"}
 
+    # Trace side of the prover (BASELINE configs[3] trace length): 2^16 trace
+    # -> iNTT -> coset LDE 2^19 -> Merkle commit, device-resident (reported
+    # beside the metric, never `value`).
+    trace_stage = None
+    if world == 1 and log_n >= 19:
+        tr = _coeffs(7, 1 << 16, fri_amd.P)
+        ctx.trace_commit(tr, 3)
+        k = 10
+        t0 = time.perf_counter()
+        for _ in range(k):
+            ctx.trace_commit(tr, 3)
+        trace_stage = {"ms_per_call": round(1000.0 * (time.perf_counter() - t0) / k, 4),
+                       "what": "fri_trace_commit: 2^16 trace -> iNTT -> LDE on 5*<w_2^19> -> SHA-256 Merkle "
+                               "(host trace in, root + coefficients + LDE read back)"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = _cpu_baseline(coeffs, d, log_n)
@@ -304,6 +319,7 @@ def main():
             "whole_commit": whole,
             "breakdown_ms_per_step": breakdown,
             "pcie_inclusive": pcie,
+            "prover_trace_commit": trace_stage,
             "cpu_baseline": cpu,
         }
         if note:

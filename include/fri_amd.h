@@ -127,6 +127,17 @@ int fri_fold(fri_ctx* ctx, const uint32_t* layer, uint32_t log_m, uint32_t layer
  * `root() -> String` is their lowercase hex.  n must be >= 1. */
 int fri_merkle_root(fri_ctx* ctx, const uint32_t* values, size_t n, uint8_t root32[32]);
 
+/* Trace side of the prover (the reference's src/trace and src/prover are
+ * empty): interpolate 2^log_t trace values on the subgroup
+ * <w_{2^log_t}> (Polynomial::interpolate, src/polynomial/ops.rs:239-241),
+ * evaluate the polynomial on the coset offset*<w_n>, n = 2^(log_t+log_blowup)
+ * (the low-degree extension), and Merkle-commit the LDE (merkle/mod.rs:10-26).
+ * root32 = LDE tree root.  Optional: coeffs_out (2^log_t entries, *coeff_len
+ * = trimmed length), lde_out (n entries).  The tree stays on the device. */
+int fri_trace_commit(fri_ctx* ctx, const uint32_t* trace, uint32_t log_t, uint32_t log_blowup,
+                     uint32_t offset, uint8_t root32[32], uint32_t* coeffs_out, size_t* coeff_len,
+                     uint32_t* lde_out);
+
 /* ---------------------------------------------------------- FRI commit */
 /* Full FRI commit — fri_commit(poly, domain, &mut channel)
  * (src/fri/fri_commit.rs:72-122): LDE of `coeffs` on offset*<w_n>,

@@ -99,6 +99,8 @@ struct fri_ctx {
     hipEvent_t ev_vals = nullptr, ev_xchg = nullptr;
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
     uint32_t* dq_buf = nullptr;     // decommitment gather staging (64 KiB)
+    uint32_t* trace_tree = nullptr; // Merkle tree of the last fri_trace_commit LDE
+    size_t trace_tree_cap = 0;      // leaves it can hold
 };
 
 #define FRI_HIP(ctx, expr)                                                              \
@@ -220,6 +222,7 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     hipFree(ctx->pow_lo); hipFree(ctx->pow_hi);
     hipFree(ctx->d_state);
     hipFree(ctx->dq_buf);
+    hipFree(ctx->trace_tree);
     if (ctx->h_state) hipHostFree(ctx->h_state);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -353,6 +356,67 @@ __global__ void k_level_generic(const uint32_t* in, uint32_t* out, size_t cnt) {
     if (j >= pc) return;
     if (2 * j + 1 < cnt) sha::node(in + 16 * j, in + 16 * j + 8, out + 8 * j);
     else for (int i = 0; i < 8; i++) out[8 * j + i] = in[16 * j + i];
+}
+
+// Trace side of the prover (the reference's
+// src/trace and src/prover are empty): interpolate the trace on its subgroup
+// <w_t> (Polynomial::interpolate, ops.rs:239 -> interpolation.rs:121-152),
+// evaluate it on the blown-up coset offset*<w_n> (the LDE, as
+// fri_commit.rs:78 evaluates), and Merkle-commit the LDE (merkle/mod.rs:10-26),
+// all device-resident.  The LDE tree stays in the context (trace_tree).
+extern "C" int fri_trace_commit(fri_ctx* ctx, const uint32_t* trace, uint32_t log_t, uint32_t log_blowup,
+                                uint32_t offset, uint8_t root32[32], uint32_t* coeffs_out, size_t* coeff_len,
+                                uint32_t* lde_out) {
+    if (!ctx || !trace || !root32) return fail(ctx, FRI_EINVAL, "null argument");
+    const uint32_t L = log_t + log_blowup;
+    if (L > ctx->log_n_max || L < 1) return fail(ctx, FRI_EINVAL, "log_t + log_blowup out of range for context");
+    if (offset == 0 || offset >= P) return fail(ctx, FRI_EINVAL, "offset must be a nonzero canonical element");
+    const size_t nt = (size_t)1 << log_t, n = (size_t)1 << L;
+    if (!check_canonical(trace, nt)) return fail(ctx, FRI_EINVAL, "trace value not canonical (>= p)");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    if (ctx->trace_tree_cap < n) {
+        hipFree(ctx->trace_tree);
+        ctx->trace_tree = nullptr;
+        ctx->trace_tree_cap = 0;
+        FRI_HIP(ctx, hipMalloc(&ctx->trace_tree, (n * 2) * 32));
+        ctx->trace_tree_cap = n;
+    }
+    hipStream_t s = ctx->stream;
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, trace, nt * 4, hipMemcpyHostToDevice, s));
+    // coefficients: c_j = nt^-1 sum_i trace_i w_t^-ij
+    NttPlan ip{};
+    ip.log_n = log_t;
+    ip.tw = ctx->tw_inv;
+    launch_pow_table(ctx->pow_lo, ctx->pow_hi, log_t, 1u, inv_std((uint32_t)(nt % P)), s);
+    ip.post_lo = ctx->pow_lo;
+    ip.post_hi = ctx->pow_hi;
+    launch_ntt(ip, ctx->scratch_a, nt, ctx->scratch_b, s);
+    // LDE on offset * <w_n>
+    NttPlan lp = lde_plan(ctx, L);
+    launch_pow_table(ctx->pow_lo, ctx->pow_hi, L, offset, 1u, s);
+    lp.pre_lo = ctx->pow_lo;
+    lp.pre_hi = ctx->pow_hi;
+    launch_ntt(lp, ctx->scratch_b, nt, ctx->scratch_c, s);
+    // Merkle tree of the LDE, every level kept
+    LayerTask t{};
+    t.values = ctx->scratch_c;
+    t.tree = ctx->trace_tree;
+    t.L = L;
+    launch_layer(t, s);
+    FRI_HIP(ctx, hipGetLastError());
+    uint32_t w[8];
+    FRI_HIP(ctx, hipMemcpyAsync(w, ctx->trace_tree + 8 * level_offset(L, L), 32, hipMemcpyDeviceToHost, s));
+    if (coeffs_out) FRI_HIP(ctx, hipMemcpyAsync(coeffs_out, ctx->scratch_b, nt * 4, hipMemcpyDeviceToHost, s));
+    if (lde_out) FRI_HIP(ctx, hipMemcpyAsync(lde_out, ctx->scratch_c, n * 4, hipMemcpyDeviceToHost, s));
+    FRI_HIP(ctx, hipStreamSynchronize(s));
+    digest_to_bytes(w, root32);
+    if (coeffs_out && coeff_len) {
+        size_t len = nt;
+        while (len > 0 && coeffs_out[len - 1] == 0) len--;      // Polynomial::new trim (ops.rs:19-37)
+        *coeff_len = len;
+    }
+    ctx->err.clear();
+    return FRI_OK;
 }
 
 extern "C" int fri_merkle_root(fri_ctx* ctx, const uint32_t* values, size_t n, uint8_t root32[32]) {

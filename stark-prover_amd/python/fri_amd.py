@@ -101,6 +101,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_layer_copy": (i32, [vp, u32, pu32, sz]),
         "fri_tree_level_copy": (i32, [vp, u32, u32, ctypes.c_char_p, sz]),
         "fri_auth_path": (i32, [vp, u32, ctypes.c_uint64, pu32, ctypes.c_char_p, ctypes.POINTER(u32)]),
+        "fri_trace_commit": (i32, [vp, pu32, u32, u32, u32, ctypes.c_char_p, pu32, ctypes.POINTER(sz), pu32]),
         "fri_decommit_query": (i32, [vp, ctypes.c_uint64, pu32, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]),
         "fri_set_profiling": (i32, [vp, i32]),
         "fri_get_profile": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -244,6 +245,21 @@ class Context:
         dep = ctypes.c_uint32()
         self._check(self.lib.fri_auth_path(self.h, k, index, ctypes.byref(val), buf, ctypes.byref(dep)))
         return val.value, [buf.raw[32 * i: 32 * i + 32] for i in range(dep.value)]
+
+    def trace_commit(self, trace, log_blowup: int, offset: int = GENERATOR):
+        """fri_trace_commit: (LDE Merkle root bytes, trimmed trace-polynomial
+        coefficients, LDE values) for 2^log_t trace values."""
+        tr = _u32(trace)
+        log_t = tr.size.bit_length() - 1
+        if tr.size != 1 << log_t:
+            raise FriError(FRI_EINVAL, "trace length must be a power of two")
+        coeffs = np.empty(tr.size, dtype=np.uint32)
+        lde = np.empty(tr.size << log_blowup, dtype=np.uint32)
+        root = ctypes.create_string_buffer(32)
+        ln = ctypes.c_size_t()
+        self._check(self.lib.fri_trace_commit(self.h, _ptr(tr), log_t, log_blowup, offset, root, _ptr(coeffs),
+                                              ctypes.byref(ln), _ptr(lde)))
+        return root.raw, coeffs[: ln.value], lde
 
     def decommit_query(self, index: int, n_layers: int, log_n: int):
         """fri_decommit_query: per committed layer k, (value[idx], value[sib],

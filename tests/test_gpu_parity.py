@@ -404,3 +404,55 @@ def test_decommit_errors(ctx):
                                     ctypes.byref(ln))
     assert rc == fri_amd.FRI_EINVAL                            # no paths buffer ...
     assert ln.value == sum(64 * (7 - k) for k in range(5))     # ... but the size is reported (5 layers)
+
+
+# ---- trace side of the prover: fri_trace_commit -------
+def _stark101_trace(n):
+    """STARK-101's FibonacciSq trace: a0 = 1, a1 = 3141592, a_{i+2} = a_{i+1}^2 + a_i^2 (mod p)."""
+    a = [1, 3141592]
+    while len(a) < n:
+        a.append((a[-1] * a[-1] + a[-2] * a[-2]) % P)
+    return a[:n]
+
+
+def test_trace_commit_small_vs_reference_algorithms(ctx, oracle):
+    """Lagrange interpolation + Horner evaluation + rs_merkle tree (the
+    reference's own algorithms, restated) at 2^6 -> 2^9."""
+    log_t, lb = 6, 3
+    trace = oracle.splitmix64_field(77, 1 << log_t)
+    root, coeffs, lde = ctx.trace_commit(trace, lb)
+    xs = oracle.coset_domain(log_t, offset=1)
+    want_c = oracle.interpolate_lagrange_polynomials(xs, trace, P)
+    assert [int(c) for c in coeffs] == want_c
+    want_lde = [oracle.poly_evaluate(want_c, x, P) for x in oracle.coset_domain(log_t + lb)]
+    assert [int(v) for v in lde] == want_lde
+    assert root == oracle.merkle_levels(want_lde)[-1][0]
+
+
+@pytest.mark.parametrize("log_t,lb,kind", [(10, 3, "stark101"), (16, 3, "random"), (16, 2, "stark101")])
+def test_trace_commit_vs_fast_oracle(ctx, corc, oracle, log_t, lb, kind):
+    """BASELINE configs[3]'s trace length (2^16) and the STARK-101 trace, vs
+    the C oracle's coset interpolation, LDE and Merkle build, plus a round
+    trip: every 2^lb-th LDE point lies on offset*<w_t>, and interpolating
+    those values gives the trace polynomial back."""
+    nt = 1 << log_t
+    trace = _stark101_trace(nt) if kind == "stark101" else oracle.splitmix64_field(log_t, nt)
+    root, coeffs, lde = ctx.trace_commit(trace, lb)
+    ys = np.ascontiguousarray(np.array(trace, dtype=np.uint64))
+    oc = np.zeros(nt, dtype=np.uint64)
+    ln = corc.orc_interpolate_coset(ys.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), log_t, 1, 5, P,
+                                    oc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    assert ln == len(coeffs) and np.array_equal(oc[:ln].astype(np.uint32), coeffs)
+    ol = np.zeros(nt << lb, dtype=np.uint64)
+    c64 = np.ascontiguousarray(oc[:max(ln, 1)])
+    assert corc.orc_lde(c64.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), ln, log_t + lb, 5, 5, P,
+                        ol.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) == 0
+    assert np.array_equal(ol.astype(np.uint32), lde)
+    cnt = corc.orc_merkle_nodes_count(nt << lb)
+    buf = ctypes.create_string_buffer(32 * cnt)
+    corc.orc_merkle_build(ol.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), nt << lb, buf)
+    assert root == buf.raw[32 * (cnt - 1):]
+    # every 2^lb-th LDE point is offset * w_t^i: interpolating those values on
+    # that coset gives the trace polynomial back
+    back = ctx.interpolate(lde[:: 1 << lb], 5)
+    assert np.array_equal(back, coeffs)
