@@ -1056,23 +1056,44 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     else if (dev_coeffs && dev_coeffs != p.d_in && d)
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, s));
 
-    // ---- layer 0: coset LDE slice evals[rank + G*m] ---------------------
-    const uint32_t sft = mul_std(offset, pow_std(root_of_unity(log_n), rank));   // s = offset * w_n^rank
-    size_t sp = span_begin(ctx, "lde", d * 4 + M * 8);
-    launch_coset_coeffs(p.d_in, d, db.recv, M, pow_std(sft, M), s);              // P mod (x^M - s^M)
-    launch_pow_table(db.pre_lo, db.pre_hi, log_n - logG, sft, 1u, s);
-    NttPlan np{};
-    np.log_n = log_n - logG;
-    np.tw = ctx->tw_fwd;
-    np.pre_lo = db.pre_lo;
-    np.pre_hi = db.pre_hi;
-    launch_ntt(np, db.recv, M, db.cyc, s);
-    span_end(ctx, sp);
-    sp = span_begin(ctx, "alltoall", M * 4);
-    rc = tp_alltoall(ctx, db.cyc, db.recv, (M / G) * 4, s);                       // coset slices -> blocks
-    if (rc) return rc;
-    launch_cyclic_to_block(db.recv, p.layers + p.layer_off[0], M, G, s);
-    span_end(ctx, sp);
+    size_t sp;
+    if (G == 2) {
+        // ---- layer 0, two ranks: radix-2 decimation, no exchange ---------
+        // P(offset w_n^(bM+j)) = E(offset^2 w_M^j) + (-1)^b offset w_n^j O(offset^2 w_M^j):
+        // both size-M NTTs on every rank, then this rank's block.
+        sp = span_begin(ctx, "lde", d * 4 + M * 12);
+        const size_t de = (d + 1) / 2, dod = d / 2;
+        launch_decimate(p.d_in, d, ctx->scratch_a, ctx->scratch_b, s);
+        launch_pow_table(db.pre_lo, db.pre_hi, log_n - 1, mul_std(offset, offset), 1u, s);
+        NttPlan np{};
+        np.log_n = log_n - 1;
+        np.tw = ctx->tw_fwd;
+        np.pre_lo = db.pre_lo;
+        np.pre_hi = db.pre_hi;
+        launch_ntt(np, ctx->scratch_a, de, db.cyc, s);
+        launch_ntt(np, ctx->scratch_b, dod, db.recv, s);
+        launch_pow_table(ctx->pow_lo, ctx->pow_hi, log_n - 1, root_of_unity(log_n), offset, s);   // offset * w_n^j
+        launch_radix2_block(db.cyc, db.recv, ctx->pow_lo, ctx->pow_hi, p.layers + p.layer_off[0], M, rank, s);
+        span_end(ctx, sp);
+    } else {
+        // ---- layer 0: coset LDE slice evals[rank + G*m] -------------------
+        const uint32_t sft = mul_std(offset, pow_std(root_of_unity(log_n), rank));   // s = offset * w_n^rank
+        sp = span_begin(ctx, "lde", d * 4 + M * 8);
+        launch_coset_coeffs(p.d_in, d, db.recv, M, pow_std(sft, M), s);              // P mod (x^M - s^M)
+        launch_pow_table(db.pre_lo, db.pre_hi, log_n - logG, sft, 1u, s);
+        NttPlan np{};
+        np.log_n = log_n - logG;
+        np.tw = ctx->tw_fwd;
+        np.pre_lo = db.pre_lo;
+        np.pre_hi = db.pre_hi;
+        launch_ntt(np, db.recv, M, db.cyc, s);
+        span_end(ctx, sp);
+        sp = span_begin(ctx, "alltoall", M * 4);
+        rc = tp_alltoall(ctx, db.cyc, db.recv, (M / G) * 4, s);                       // coset slices -> blocks
+        if (rc) return rc;
+        launch_cyclic_to_block(db.recv, p.layers + p.layer_off[0], M, G, s);
+        span_end(ctx, sp);
+    }
 
     std::vector<uint32_t> block_of(G), rank_of(G);
     for (uint32_t r = 0; r < G; r++) block_of[r] = rank_of[r] = r;

@@ -60,6 +60,34 @@ void launch_pair_fold(const uint32_t* first, const uint32_t* second, const uint3
                        st, r);
 }
 
+// G = 2, layer 0 without an all-to-all (radix-2 decimation): even/odd
+// coefficients for two size-M NTTs ...
+__global__ void k_decimate(const uint32_t* __restrict__ a, size_t d, uint32_t* __restrict__ ev,
+                           uint32_t* __restrict__ od) {
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (2 * k < d) ev[k] = a[2 * k];
+    if (2 * k + 1 < d) od[k] = a[2 * k + 1];
+}
+void launch_decimate(const uint32_t* a, size_t d, uint32_t* ev, uint32_t* od, hipStream_t s) {
+    const size_t h = (d + 1) / 2;
+    if (h) hipLaunchKernelGGL(k_decimate, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, s, a, d, ev, od);
+}
+// ... and the block of rank b:  L0[j] = E[j] + (-1)^b * offset * w_n^j * O[j],
+// tw = pow table of offset * w_n^j (Montgomery lo/hi split).
+__global__ void k_radix2_block(const uint32_t* __restrict__ E, const uint32_t* __restrict__ O,
+                               const uint32_t* __restrict__ tlo, const uint32_t* __restrict__ thi,
+                               uint32_t* __restrict__ out, size_t M, uint32_t negate) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= M) return;
+    const uint32_t t = mmul(mmul(O[j], thi[j >> POW_LO_LOG]), tlo[j & ((1u << POW_LO_LOG) - 1)]);
+    out[j] = negate ? sub(E[j], t) : add(E[j], t);
+}
+void launch_radix2_block(const uint32_t* E, const uint32_t* O, const uint32_t* tlo, const uint32_t* thi,
+                         uint32_t* out, size_t M, uint32_t negate, hipStream_t s) {
+    hipLaunchKernelGGL(k_radix2_block, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, E, O, tlo, thi, out, M,
+                       negate);
+}
+
 struct Perm64 { uint32_t p[64]; };
 // dst digest block_of_rank[r] <- src digest r  (G <= 64)
 __global__ void k_permute_digests(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t G, Perm64 pm) {

@@ -107,6 +107,9 @@ void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end = nu
 void launch_coef(const LayerTask& t, uint32_t G, hipStream_t s);
 // fri_dist_kernels.hip
 void launch_coset_coeffs(const uint32_t* a, size_t d, uint32_t* out, size_t M, uint32_t c_std, hipStream_t s);
+void launch_decimate(const uint32_t* a, size_t d, uint32_t* ev, uint32_t* od, hipStream_t s);
+void launch_radix2_block(const uint32_t* E, const uint32_t* O, const uint32_t* tlo, const uint32_t* thi,
+                         uint32_t* out, size_t M, uint32_t negate, hipStream_t s);
 void launch_cyclic_to_block(const uint32_t* recv, uint32_t* block, size_t B, uint32_t G, hipStream_t s);
 void launch_pair_fold(const uint32_t* first, const uint32_t* second, const uint32_t* xinv, uint32_t* out, size_t h,
                       const DevState* st, int r, hipStream_t s);
