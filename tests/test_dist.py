@@ -46,7 +46,7 @@ def single_node(oracle, log_n, seed):
             "final_degree": r.final_degree, "state": ch.state}
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_protocol_model_gloo(oracle, world):
     log_n = 10
     want = single_node(oracle, log_n, 42)
@@ -60,6 +60,7 @@ def test_sharded_protocol_model_gloo(oracle, world):
     (2, 22, 3), (4, 22, 3),          # several sharded layers, then local
     (2, 20, 3), (2, 21, 3),          # switch to local right after layer 0 / 1
     (2, 21, 1), (4, 22, 0),          # d > n/G: the coset reduction folds several chunks
+    (8, 23, 3),                      # the driver's N = 8 shape: 3-level top, block permutations
 ])
 def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, corc, oracle):
     import ctypes
