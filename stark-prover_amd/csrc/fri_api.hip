@@ -97,6 +97,8 @@ struct fri_ctx {
     DistBuf db;
     hipStream_t xstream = nullptr;  // exchange stream (overlaps the local tree)
     hipEvent_t ev_vals = nullptr, ev_xchg = nullptr;
+    hipStream_t cstream = nullptr;  // coefficient-fold stream (overlaps the local tree)
+    hipEvent_t ev_pre = nullptr, ev_coef = nullptr;
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
     uint32_t* dq_buf = nullptr;     // decommitment gather staging (64 KiB)
     uint32_t* trace_tree = nullptr; // Merkle tree of the last fri_trace_commit LDE
@@ -217,6 +219,9 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     if (ctx->xstream) hipStreamDestroy(ctx->xstream);
     if (ctx->ev_vals) hipEventDestroy(ctx->ev_vals);
     if (ctx->ev_xchg) hipEventDestroy(ctx->ev_xchg);
+    if (ctx->cstream) hipStreamDestroy(ctx->cstream);
+    if (ctx->ev_pre) hipEventDestroy(ctx->ev_pre);
+    if (ctx->ev_coef) hipEventDestroy(ctx->ev_coef);
     hipFree(ctx->tw_fwd); hipFree(ctx->tw_inv);
     hipFree(ctx->scratch_a); hipFree(ctx->scratch_b); hipFree(ctx->scratch_c);
     hipFree(ctx->pow_lo); hipFree(ctx->pow_hi);
@@ -1017,6 +1022,11 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
         FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_vals, hipEventDisableTiming));
         FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_xchg, hipEventDisableTiming));
     }
+    if (!ctx->cstream) {
+        FRI_HIP(ctx, hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
+        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_pre, hipEventDisableTiming));
+        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_coef, hipEventDisableTiming));
+    }
     (void)G;
     return FRI_OK;
 }
@@ -1132,13 +1142,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         size_t spl = (k == 0 && tl.L >= 19) ? span_begin(ctx, "merkle_layer0_leaf", ((uint64_t)4 << tl.L) + 32 * leaf_nodes)
                                             : (size_t)-1;
         size_t spk = span_begin(ctx, k == 0 ? "layer0" : "layers", 0);
-        launch_layer(tl, s, spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
-        // all-gather block roots -> block order -> top tree level 0
-        rc = tp_allgather(ctx, tl.tree + 8 * level_offset(tl.L, tl.L), db.roots, 32, s);
-        if (rc) return rc;
-        uint32_t* top = db.top + (size_t)k * 2 * 64 * 8;
-        launch_permute_digests(db.roots, top, G, block_of.data(), s);
-        // coefficient task of this layer (redundant on every rank) + top + channel
+        // coefficient task of this layer (redundant on every rank; needs only
+        // round k-1's beta): on its own stream, concurrent with the block tree
         LayerTask tc{};
         tc.k = k;
         tc.coef_in = k ? coef_buf(p, k - 1) : p.d_in;
@@ -1150,7 +1155,21 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         uint32_t Gc = (uint32_t)((clen + 8191) / 8192);
         if (Gc < 1) Gc = 1;
         if (Gc > 2048) Gc = 2048;
-        launch_coef(tc, Gc, s);
+        const bool side = !ctx->profiling;   // (profiled commits keep one stream for the spans)
+        if (side) {
+            FRI_HIP(ctx, hipEventRecord(ctx->ev_pre, s));
+            FRI_HIP(ctx, hipStreamWaitEvent(ctx->cstream, ctx->ev_pre, 0));
+            launch_coef(tc, Gc, ctx->cstream);
+            FRI_HIP(ctx, hipEventRecord(ctx->ev_coef, ctx->cstream));
+        }
+        launch_layer(tl, s, spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
+        // all-gather block roots -> block order -> top tree level 0
+        rc = tp_allgather(ctx, tl.tree + 8 * level_offset(tl.L, tl.L), db.roots, 32, s);
+        if (rc) return rc;
+        uint32_t* top = db.top + (size_t)k * 2 * 64 * 8;
+        launch_permute_digests(db.roots, top, G, block_of.data(), s);
+        if (side) FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_coef, 0));
+        else launch_coef(tc, Gc, s);
         LayerTask tt = tc;
         tt.tree = top;
         tt.L = logG;
