@@ -475,6 +475,101 @@ def decommit_fri(num_queries: int, max_index: int, proof: "FRIProof", channel: C
         decommit_fri_layers(idx, proof, channel)
 
 
+def _merkle_path_ok(value: int, index: int, path: bytes, depth: int, root: bytes) -> bool:
+    """rs_merkle single-leaf proof of a power-of-two tree: siblings leaf -> root."""
+    if len(path) != 32 * depth:
+        return False
+    h = hashlib.sha256(value.to_bytes(8, "big")).digest()              # merkle/mod.rs:14-15
+    for lvl in range(depth):
+        sib = path[32 * lvl:32 * lvl + 32]
+        h = hashlib.sha256(sib + h if (index >> lvl) & 1 else h + sib).digest()
+    return h == root
+
+
+def verify_fri(messages: Sequence[bytes], log_n: int, n_layers: int, num_queries: int, max_index: int,
+               offset: int = GENERATOR, channel_state: str = "") -> bool:
+    """Check a FRI transcript: the proof messages that fri_commit followed by
+    decommit_fri append to Channel.proof (fri_commit.rs:72-179).
+
+    The reference's verify_fri (src/fri/fri_verify.rs:12-177) is a sketch.
+    It re-reads proof.last() and leaves the fold check as a placeholder, so
+    this is the check it outlines, made complete:
+      * replay a fresh channel from ``channel_state``: every root is sent;
+        every beta and query index must be the one the replay draws; the
+        final value is sent;
+      * every authentication path must lead to its layer's root;
+      * every layer k >= 1 value must equal the fold of its two parents:
+        (a + b)/2 + beta (a - b) / (2 x);
+      * the last layer must hold the final constant.
+    ``n_layers`` = number of committed layers (the reference's
+    expected_num_layers). Returns False on any mismatch or malformed transcript.
+    """
+    msgs = list(messages)
+    pos = 0
+
+    def take():
+        nonlocal pos
+        if pos >= len(msgs):
+            raise ValueError("transcript ended early")
+        pos += 1
+        return msgs[pos - 1]
+
+    try:
+        ch = Channel(state=channel_state)
+        roots, betas = [], []
+        for k in range(n_layers):
+            r = take()
+            if len(r) != 64:
+                return False
+            roots.append(bytes.fromhex(r.decode()))
+            ch.send(r)
+            if k < n_layers - 1:
+                beta = ch.receive_random_field_element()
+                if take() != beta.to_bytes(8, "big"):
+                    return False
+                betas.append(beta)
+        fin = take()
+        if len(fin) != 8:
+            return False
+        final = int.from_bytes(fin, "big")
+        ch.send(fin)
+        inv2 = pow(2, P - 2, P)
+        for _ in range(num_queries):
+            idx = ch.receive_random_int(0, max_index, True)
+            if take() != idx.to_bytes(8, "big"):
+                return False
+            prev = None                                  # (value at i, value at i + m/2, i, m) of layer k-1
+            for k in range(n_layers):
+                m = 1 << (log_n - k)
+                depth = log_n - k
+                if m == 1:
+                    extra = take()
+                    ch.send(extra)
+                i = idx % m
+                sib = (i + m // 2) % m
+                vb, path, sb, spath = take(), take(), take(), take()
+                for msg in (vb, path, sb, spath):
+                    ch.send(msg)
+                v, sv = int.from_bytes(vb, "big"), int.from_bytes(sb, "big")
+                if v >= P or sv >= P:
+                    return False
+                if not (_merkle_path_ok(v, i, path, depth, roots[k]) and _merkle_path_ok(sv, sib, spath, depth, roots[k])):
+                    return False
+                if prev is not None:
+                    pa, pb, pj, pm = prev                    # pa = L[pj], pb = L[pj + pm/2]
+                    x = pow(offset, 1 << (k - 1), P) * pow(pow(GENERATOR, (P - 1) // pm, P), pj, P) % P
+                    fold = ((pa + pb) + betas[k - 1] * (pa - pb) % P * pow(x, P - 2, P)) % P * inv2 % P
+                    if fold != v:
+                        return False
+                j = i % (m // 2) if m > 1 else 0
+                prev = (v, sv, j, m) if i < m // 2 or m == 1 else (sv, v, j, m)
+                if k == n_layers - 1 and (v != final or sv != final):
+                    return False
+        return pos == len(msgs)
+    except (ValueError, IndexError, UnicodeDecodeError):
+        return False
+
+
 _CTX_CACHE = {}
 
 

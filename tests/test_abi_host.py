@@ -122,3 +122,44 @@ def test_bench_algorithmic_bytes_match_survey():
     bf, bt = bench.algorithmic_bytes(20, 1 << 17)
     assert abs((bf + bt) / 1e9 - 0.152) < 0.002
     assert bench.sha_compressions(24, 1 << 21) > 1.0e8
+
+
+# ---- verify_fri (host mirror) on oracle-produced transcripts -------------
+def _oracle_transcript(oracle, coeffs, log_n, queries, state="", offset=5):
+    ch = oracle.Channel(state=state)
+    r = oracle.fri_commit(coeffs, log_n, ch, offset=offset)
+    oracle.decommit_fri(queries, (1 << log_n) - 1, r.layers, r.trees, ch)
+    return ch.proof, len(r.roots)
+
+
+def test_verify_fri_accepts_golden_transcripts(oracle, golden):
+    import fri_amd
+    for c in golden["cases"]:
+        if c["forced_betas"] is not None:
+            continue
+        msgs, n_layers = _oracle_transcript(oracle, c["coeffs"], c["log_n"], 3, c["channel_in"], c["offset"])
+        assert fri_amd.verify_fri(msgs, c["log_n"], n_layers, 3, (1 << c["log_n"]) - 1, c["offset"],
+                                  c["channel_in"]), c["name"]
+
+
+def test_verify_fri_rejects_tampering(oracle):
+    import fri_amd
+    log_n = 9
+    msgs, n_layers = _oracle_transcript(oracle, oracle.splitmix64_field(5, 64), log_n, 4)
+    args = (log_n, n_layers, 4, (1 << log_n) - 1)
+    assert fri_amd.verify_fri(msgs, *args)
+    n_commit = 2 * n_layers                       # roots + betas + final value
+    rng = __import__("random").Random(1)
+    for trial in range(40):
+        bad = list(msgs)
+        i = rng.randrange(len(bad))
+        if len(bad[i]) == 0:
+            continue
+        b = bytearray(bad[i])
+        j = rng.randrange(len(b))
+        b[j] ^= 1 << rng.randrange(8)
+        bad[i] = bytes(b)
+        assert not fri_amd.verify_fri(bad, *args), (trial, i, i < n_commit)
+    assert not fri_amd.verify_fri(msgs[:-1], *args)            # truncated
+    assert not fri_amd.verify_fri(msgs + [b"x"], *args)        # trailing garbage
+    assert not fri_amd.verify_fri(msgs, log_n, n_layers, 4, (1 << log_n) - 2)   # other query indices

@@ -456,3 +456,17 @@ def test_trace_commit_vs_fast_oracle(ctx, corc, oracle, log_t, lb, kind):
     # that coset gives the trace polynomial back
     back = ctx.interpolate(lde[:: 1 << lb], 5)
     assert np.array_equal(back, coeffs)
+
+
+def test_verify_fri_on_device_transcript(ctx):
+    """End to end at 2^20: GPU commit + GPU decommitment gather verify."""
+    import fri_amd
+    log_n = 20
+    coeffs = np.array(__import__("fri_oracle").splitmix64_field(11, 1 << 17), dtype=np.uint64)
+    ch = fri_amd.Channel()
+    proof = fri_amd.fri_commit(coeffs, log_n, ch, ctx=ctx)
+    fri_amd.decommit_fri(8, (1 << log_n) - 1, proof, ch)
+    assert fri_amd.verify_fri(ch.proof, log_n, proof.n_layers, 8, (1 << log_n) - 1)
+    bad = list(ch.proof)
+    bad[-3] = bytes([bad[-3][0] ^ 1]) + bad[-3][1:]          # a sibling value of the last query
+    assert not fri_amd.verify_fri(bad, log_n, proof.n_layers, 8, (1 << log_n) - 1)
