@@ -1,0 +1,462 @@
+// stark101.cpp — host side of the C++ mirror (see stark101.hpp).  Everything
+// field-sized on the commit path goes through libfri_amd.so; this file holds
+// the transcript (SHA-256 on the host, as the reference's Channel does it),
+// argument checks that reproduce the reference's panics, and the glue that
+// turns fri_commit_result into Channel messages and an FRIProof.
+#include "stark101.hpp"
+
+#include <cstdio>
+#include <cstring>
+#include <random>
+
+namespace stark101 {
+
+// ------------------------------------------------------------------ SHA-256
+namespace {
+constexpr uint32_t K256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+void compress(uint32_t h[8], const uint8_t blk[64]) {
+    uint32_t w[64];
+    for (int i = 0; i < 16; i++)
+        w[i] = (uint32_t)blk[4 * i] << 24 | (uint32_t)blk[4 * i + 1] << 16 | (uint32_t)blk[4 * i + 2] << 8 | blk[4 * i + 3];
+    for (int i = 16; i < 64; i++) {
+        uint32_t s0 = rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
+        uint32_t s1 = rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
+        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
+    for (int i = 0; i < 64; i++) {
+        uint32_t t1 = k + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + K256[i] + w[i];
+        uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
+}
+}  // namespace
+
+namespace sha {
+std::array<uint8_t, 32> digest(const uint8_t* data, size_t len) {
+    uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    size_t full = len / 64;
+    for (size_t i = 0; i < full; i++) compress(h, data + 64 * i);
+    uint8_t tail[128] = {0};
+    size_t rem = len - 64 * full;
+    if (rem) std::memcpy(tail, data + 64 * full, rem);
+    tail[rem] = 0x80;
+    size_t tl = rem + 9 <= 64 ? 64 : 128;
+    uint64_t bits = static_cast<uint64_t>(len) * 8;
+    for (int i = 0; i < 8; i++) tail[tl - 1 - i] = static_cast<uint8_t>(bits >> (8 * i));
+    compress(h, tail);
+    if (tl == 128) compress(h, tail + 64);
+    std::array<uint8_t, 32> out{};
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 4; j++) out[4 * i + j] = static_cast<uint8_t>(h[i] >> (24 - 8 * j));
+    return out;
+}
+
+std::string hex(const uint8_t* data, size_t len) {
+    static const char* d = "0123456789abcdef";
+    std::string s(2 * len, '0');
+    for (size_t i = 0; i < len; i++) {
+        s[2 * i] = d[data[i] >> 4];
+        s[2 * i + 1] = d[data[i] & 15];
+    }
+    return s;
+}
+
+std::string digest_hex(const std::string& s) {
+    auto dg = digest(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    return hex(dg.data(), dg.size());
+}
+
+std::vector<uint8_t> from_hex(const std::string& s) {
+    if (s.size() % 2) throw Panic("odd-length hex string");
+    auto nib = [](char c) -> int {
+        if (c >= '0' && c <= '9') return c - '0';
+        if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+        if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+        throw Panic("invalid hex digit");
+    };
+    std::vector<uint8_t> out(s.size() / 2);
+    for (size_t i = 0; i < out.size(); i++) out[i] = static_cast<uint8_t>(nib(s[2 * i]) << 4 | nib(s[2 * i + 1]));
+    return out;
+}
+}  // namespace sha
+
+uint64_t os_random_u64() {
+    static thread_local std::random_device rd;      // OsRng (element.rs:32-36)
+    return (static_cast<uint64_t>(rd()) << 32) ^ rd();
+}
+
+FE omega(uint32_t log_n) {
+    if (log_n > 30) throw Panic("no subgroup of order 2^" + std::to_string(log_n));
+    return FE(FRI_GENERATOR).pow((P - 1) >> log_n);
+}
+
+// ---------------------------------------------------------------------- Gpu
+Gpu::Gpu(int device, uint32_t log_n_max) : log_n_max_(log_n_max) {
+    int rc = fri_ctx_create(device, log_n_max, &ctx_);
+    if (rc != FRI_OK) {
+        std::string msg = ctx_ ? fri_last_error(ctx_) : "";
+        if (ctx_) fri_ctx_destroy(ctx_);
+        ctx_ = nullptr;
+        throw Panic("fri_ctx_create failed (code " + std::to_string(rc) + ")" + (msg.empty() ? "" : ": " + msg));
+    }
+}
+
+Gpu::~Gpu() {
+    if (ctx_) fri_ctx_destroy(ctx_);
+}
+
+void Gpu::check(int rc, const char* what) const {
+    if (rc != FRI_OK) throw Panic(std::string(what) + ": " + fri_last_error(ctx_) + " (code " + std::to_string(rc) + ")");
+}
+
+std::shared_ptr<Gpu> Gpu::thread_default(uint32_t log_n) {
+    static thread_local std::shared_ptr<Gpu> g;
+    const uint32_t want = log_n < 12 ? 12 : log_n;
+    if (!g || g->log_n_max() < want) g = std::make_shared<Gpu>(0, want);
+    return g;
+}
+
+namespace {
+uint32_t ceil_log2(size_t n) {
+    uint32_t l = 0;
+    while ((size_t{1} << l) < n) l++;
+    return l;
+}
+
+std::vector<uint32_t> to_u32(const std::vector<FE>& v) {
+    std::vector<uint32_t> o(v.size());
+    for (size_t i = 0; i < v.size(); i++) o[i] = static_cast<uint32_t>(v[i].value());
+    return o;
+}
+
+std::vector<FE> to_fe(const uint32_t* v, size_t n) {
+    std::vector<FE> o(n);
+    for (size_t i = 0; i < n; i++) o[i] = FE(v[i]);
+    return o;
+}
+
+// The device evaluates on offset*<omega_n>: accept exactly that domain.
+// Checks the length, D[0] = offset != 0, D[1] = offset*omega_n and the last
+// point; the remaining points are the caller's contract (coset_fri.rs:32-36),
+// as materialising and comparing 2^24 points would cost more than the commit.
+uint32_t coset_log_n(const std::vector<FE>& d, FE* offset) {
+    const size_t n = d.size();
+    if (n == 0 || (n & (n - 1))) throw Panic("domain size must be a power of two (got " + std::to_string(n) + ")");
+    const uint32_t log_n = ceil_log2(n);
+    const FE off = d[0], w = omega(log_n);
+    if (off == FE::zero()) throw Panic("domain offset must be non-zero");
+    if (n > 1 && (d[1] != off * w || d[n - 1] != off * w.pow(n - 1)))
+        throw Panic("domain is not the coset offset*<omega_n> in natural order (coset_fri.rs:32-36)");
+    *offset = off;
+    return log_n;
+}
+}  // namespace
+
+// --------------------------------------------------------------- MerkleTree
+MerkleTree::MerkleTree(const std::vector<FE>& data) {
+    if (data.empty()) throw Panic("MerkleTree of no leaves has no root (merkle/mod.rs:25)");
+    gpu_ = Gpu::thread_default(ceil_log2(data.size()));
+    auto v = to_u32(data);
+    uint8_t root[32];
+    gpu_->check(fri_merkle_root(gpu_->ctx(), v.data(), v.size(), root), "fri_merkle_root");
+    root_hex_ = sha::hex(root, 32);
+    gpu_.reset();                                     // standalone: root only
+}
+
+std::array<uint8_t, 32> MerkleTree::root_bytes() const {
+    auto b = sha::from_hex(root_hex_);
+    std::array<uint8_t, 32> r{};
+    std::memcpy(r.data(), b.data(), 32);
+    return r;
+}
+
+std::vector<uint8_t> MerkleTree::get_authentication_path(size_t index) const {
+    if (!gpu_) throw Panic("authentication paths are served by the trees of an FRIProof (standalone trees keep only the root)");
+    if (gpu_->generation() != gen_) throw Panic("FRIProof layers were replaced by a later commit on the same Gpu");
+    uint32_t value = 0, depth = 0;
+    std::vector<uint8_t> path(32 * 32);
+    gpu_->check(fri_auth_path(gpu_->ctx(), layer_, index, &value, path.data(), &depth), "fri_auth_path");
+    path.resize(32 * size_t{depth});
+    return path;
+}
+
+// ----------------------------------------------------------------- FRIProof
+bool FRIProof::resident() const { return gpu_ && gpu_->generation() == gen_; }
+
+void FRIProof::require_resident() const {
+    if (!resident()) throw Panic("FRIProof layers were replaced by a later commit on the same Gpu");
+}
+
+std::vector<FE> FRIProof::fri_layer(size_t k) const {
+    require_resident();
+    if (k >= n_layers()) throw Panic("no such FRI layer");
+    const size_t m = size_t{1} << (log_n - k);
+    std::vector<uint32_t> v(m);
+    gpu_->check(fri_layer_copy(gpu_->ctx(), static_cast<uint32_t>(k), v.data(), m), "fri_layer_copy");
+    return to_fe(v.data(), m);
+}
+
+std::vector<std::vector<FE>> FRIProof::fri_layers() const {
+    std::vector<std::vector<FE>> out;
+    for (size_t k = 0; k < n_layers(); k++) out.push_back(fri_layer(k));
+    return out;
+}
+
+// --------------------------------------------------------------- fri_commit
+FRIProof fri_commit_coset(const Poly& poly, uint32_t log_n, FE offset, FriChannel& channel,
+                          const std::shared_ptr<Gpu>& gpu) {
+    if (!gpu) throw Panic("fri_commit: no Gpu");
+    if (log_n > gpu->log_n_max()) throw Panic("fri_commit: codeword 2^" + std::to_string(log_n) + " exceeds the context");
+    std::vector<uint32_t> coeffs = to_u32(poly.coefficients);
+    fri_channel_state cin{};
+    const fri_channel_state* pin = nullptr;
+    if (!channel.state.empty()) {
+        auto st = sha::from_hex(channel.state);
+        if (st.size() != 32) throw Panic("Channel state is not a SHA-256 digest");
+        std::memcpy(cin.digest, st.data(), 32);
+        cin.has_state = 1;
+        pin = &cin;
+    }
+    fri_commit_result res{};
+    gpu->bump();                                    // previous layers are overwritten from here on
+    gpu->check(fri_commit(gpu->ctx(), coeffs.data(), coeffs.size(), log_n, static_cast<uint32_t>(offset.value()), pin,
+                          0, nullptr, &res),
+               "fri_commit");
+
+    // The channel messages the reference's loop produced (fri_commit.rs:84-114):
+    // root_hex bytes per layer, beta (8 B BE, proof only) per round, final value.
+    FRIProof proof;
+    proof.log_n = log_n;
+    proof.gpu_ = gpu;
+    proof.gen_ = gpu->generation();
+    for (uint32_t k = 0; k < res.n_layers; k++) {
+        const std::string hex = sha::hex(res.roots[k], 32);
+        std::vector<uint8_t> msg(hex.begin(), hex.end());
+        channel.proof.push_back(msg);
+        channel.compressed_proof.push_back(msg);
+        if (k < res.n_rounds) {
+            channel.proof.push_back(FriChannel::be64(res.betas[k]));
+            proof.betas.push_back(FE(res.betas[k]));
+        }
+        MerkleTree t;
+        t.root_hex_ = hex;
+        t.gpu_ = gpu;
+        t.gen_ = proof.gen_;
+        t.layer_ = k;
+        proof.fri_merkles.push_back(std::move(t));
+    }
+    auto fv = FriChannel::be64(res.final_value);
+    channel.proof.push_back(fv);
+    channel.compressed_proof.push_back(fv);
+    channel.state = res.channel_out.has_state ? sha::hex(res.channel_out.digest, 32) : "";
+    proof.final_poly = res.final_degree < 0 ? Poly::zero() : Poly({FE(res.final_value)});
+    return proof;
+}
+
+FRIProof fri_commit(Poly poly, std::vector<FE> domain, FriChannel& channel) {
+    FE offset;
+    const uint32_t log_n = coset_log_n(domain, &offset);
+    domain.clear();
+    domain.shrink_to_fit();
+    return fri_commit_coset(poly, log_n, offset, channel, Gpu::thread_default(log_n));
+}
+
+FRIProof fri_commit(const Poly& poly, const Coset& coset, FriChannel& channel) {
+    const size_t n = coset.domain_size;
+    if (n == 0 || (n & (n - 1))) throw Panic("domain size must be a power of two");
+    const uint32_t log_n = ceil_log2(n);
+    if (coset.omega != omega(log_n)) throw Panic("coset omega must be g^((p-1)/n) (frozen spec)");
+    if (coset.offset == FE::zero()) throw Panic("domain offset must be non-zero");
+    return fri_commit_coset(poly, log_n, coset.offset, channel, Gpu::thread_default(log_n));
+}
+
+// ------------------------------------------------------------------ decommit
+void decommit_fri_layers(size_t index, const FRIProof& proof, FriChannel& channel) {
+    proof.require_resident();
+    const size_t L = proof.n_layers();
+    size_t path_bytes = 0;
+    for (size_t k = 0; k < L; k++) path_bytes += 2 * 32 * (proof.log_n - k);
+    std::vector<uint32_t> values(2 * L);
+    std::vector<uint8_t> paths(path_bytes ? path_bytes : 1);
+    size_t got = 0;
+    proof.gpu_->check(fri_decommit_query(proof.gpu_->ctx(), index, values.data(), values.size(), paths.data(),
+                                         paths.size(), &got),
+                      "fri_decommit_query");
+    size_t off = 0;
+    for (size_t k = 0; k < L; k++) {
+        const size_t depth = proof.log_n - k, pb = 32 * depth;
+        std::vector<uint8_t> path(paths.begin() + off, paths.begin() + off + pb);
+        std::vector<uint8_t> spath(paths.begin() + off + pb, paths.begin() + off + 2 * pb);
+        off += 2 * pb;
+        auto v = FE(values[2 * k]).to_bytes(), sv = FE(values[2 * k + 1]).to_bytes();
+        if (depth == 0) channel.send(v);             // fri_commit.rs:147-149: length == 1 sends it first
+        channel.send(v);
+        channel.send(path);
+        channel.send(sv);
+        channel.send(spath);
+    }
+}
+
+void decommit_fri(size_t num_queries, size_t max_index, const FRIProof& proof, FriChannel& channel) {
+    for (size_t q = 0; q < num_queries; q++) {
+        const uint64_t idx = channel.receive_random_int(0, max_index, true);
+        decommit_fri_layers(idx, proof, channel);
+    }
+}
+
+// -------------------------------------------------------------------- verify
+namespace {
+bool path_ok(uint64_t value, uint64_t index, const std::vector<uint8_t>& path, size_t depth,
+             const std::array<uint8_t, 32>& root) {
+    if (path.size() != 32 * depth) return false;
+    const auto leaf = FE(value).to_bytes();                     // merkle/mod.rs:14-15
+    auto h = sha::digest(leaf.data(), 8);
+    uint8_t buf[64];
+    for (size_t lvl = 0; lvl < depth; lvl++) {
+        const uint8_t* sib = path.data() + 32 * lvl;
+        if ((index >> lvl) & 1) {
+            std::memcpy(buf, sib, 32);
+            std::memcpy(buf + 32, h.data(), 32);
+        } else {
+            std::memcpy(buf, h.data(), 32);
+            std::memcpy(buf + 32, sib, 32);
+        }
+        h = sha::digest(buf, 64);
+    }
+    return h == root;
+}
+
+uint64_t be_u64(const std::vector<uint8_t>& b) {
+    uint64_t v = 0;
+    for (uint8_t c : b) v = v << 8 | c;
+    return v;
+}
+}  // namespace
+
+bool verify_fri(const std::vector<std::vector<uint8_t>>& msgs, uint32_t log_n, size_t n_layers, size_t num_queries,
+                size_t max_index, FE offset, const std::string& channel_state) {
+    if (n_layers == 0 || n_layers > log_n + 1u) return false;
+    size_t pos = 0;
+    auto take = [&]() -> const std::vector<uint8_t>& {
+        if (pos >= msgs.size()) throw Panic("transcript ended early");
+        return msgs[pos++];
+    };
+    try {
+        FriChannel ch;
+        ch.state = channel_state;
+        std::vector<std::array<uint8_t, 32>> roots;
+        std::vector<FE> betas;
+        for (size_t k = 0; k < n_layers; k++) {
+            const auto& r = take();
+            if (r.size() != 64) return false;
+            auto rb = sha::from_hex(std::string(r.begin(), r.end()));
+            std::array<uint8_t, 32> ra{};
+            std::memcpy(ra.data(), rb.data(), 32);
+            roots.push_back(ra);
+            ch.send(r);
+            if (k + 1 < n_layers) {
+                FE beta = ch.receive_random_field_element();
+                if (take() != FriChannel::be64(beta.value())) return false;
+                betas.push_back(beta);
+            }
+        }
+        const auto& fin = take();
+        if (fin.size() != 8) return false;
+        const uint64_t final_value = be_u64(fin);
+        ch.send(fin);
+        const FE inv2 = FE(2).inverse();
+        for (size_t q = 0; q < num_queries; q++) {
+            const uint64_t idx = ch.receive_random_int(0, max_index, true);
+            if (take() != FriChannel::be64(idx)) return false;
+            bool have_prev = false;
+            uint64_t pa = 0, pb = 0, pj = 0, pm = 0;           // L[pj], L[pj + pm/2] of layer k-1
+            for (size_t k = 0; k < n_layers; k++) {
+                const size_t depth = log_n - k;
+                const uint64_t m = uint64_t{1} << depth;
+                const std::vector<uint8_t>* extra = nullptr;
+                if (m == 1) {                                    // fri_commit.rs:147-149 sends layer[0] first
+                    extra = &take();
+                    ch.send(*extra);
+                }
+                const uint64_t i = idx % m, sib = (i + m / 2) % m;
+                const auto& vb = take();
+                if (extra && *extra != vb) return false;
+                const auto& path = take();
+                const auto& sb = take();
+                const auto& spath = take();
+                for (auto* msg : {&vb, &path, &sb, &spath}) ch.send(*msg);
+                if (vb.size() != 8 || sb.size() != 8) return false;
+                const uint64_t v = be_u64(vb), sv = be_u64(sb);
+                if (v >= P || sv >= P) return false;
+                if (!path_ok(v, i, path, depth, roots[k]) || !path_ok(sv, sib, spath, depth, roots[k])) return false;
+                if (have_prev) {
+                    // x = offset^(2^(k-1)) * omega_pm^pj; fold = (a+b)/2 + beta*(a-b)/(2x)  (fri_commit.rs:32-65)
+                    const FE x = offset.pow(uint64_t{1} << (k - 1)) * omega(ceil_log2(pm)).pow(pj);
+                    const FE a(pa), b(pb);
+                    const FE fold = ((a + b) + betas[k - 1] * (a - b) * x.inverse()) * inv2;
+                    if (fold.value() != v) return false;
+                }
+                const uint64_t j = m > 1 ? i % (m / 2) : 0;
+                if (i < m / 2 || m == 1) { pa = v; pb = sv; } else { pa = sv; pb = v; }
+                pj = j;
+                pm = m;
+                have_prev = true;
+                if (k + 1 == n_layers && (v != final_value || sv != final_value)) return false;
+            }
+        }
+        return pos == msgs.size();
+    } catch (const Panic&) {
+        return false;
+    }
+}
+
+// ------------------------------------------------------- polynomial layer
+std::vector<FE> evaluate_on_coset(const Poly& poly, const Coset& coset) {
+    const size_t n = coset.domain_size;
+    if (n == 0 || (n & (n - 1))) throw Panic("domain size must be a power of two");
+    const uint32_t log_n = ceil_log2(n);
+    if (coset.omega != omega(log_n)) throw Panic("coset omega must be g^((p-1)/n) (frozen spec)");
+    auto gpu = Gpu::thread_default(log_n);
+    auto c = to_u32(poly.coefficients);
+    std::vector<uint32_t> out(n);
+    gpu->check(fri_lde(gpu->ctx(), c.data(), c.size(), log_n, static_cast<uint32_t>(coset.offset.value()), out.data()),
+               "fri_lde");
+    return to_fe(out.data(), n);
+}
+
+Poly interpolate(const std::vector<FE>& xs, const std::vector<FE>& ys) {
+    if (xs.size() != ys.size()) throw Panic("xs and ys must have the same length (interpolation.rs:127)");
+    FE offset;
+    const uint32_t log_n = coset_log_n(xs, &offset);
+    auto gpu = Gpu::thread_default(log_n);
+    auto y = to_u32(ys);
+    std::vector<uint32_t> c(xs.size());
+    size_t len = 0;
+    gpu->check(fri_interpolate(gpu->ctx(), y.data(), log_n, static_cast<uint32_t>(offset.value()), c.data(), &len),
+               "fri_interpolate");
+    return Poly(to_fe(c.data(), len));
+}
+
+std::vector<FE> batch_inverse(const std::vector<FE>& xs) {
+    if (xs.empty()) return {};
+    auto gpu = Gpu::thread_default(ceil_log2(xs.size()));
+    auto v = to_u32(xs);
+    std::vector<uint32_t> out(v.size());
+    gpu->check(fri_batch_inverse(gpu->ctx(), v.data(), out.data(), v.size()), "fri_batch_inverse");
+    return to_fe(out.data(), out.size());
+}
+
+}  // namespace stark101

@@ -542,12 +542,15 @@ def verify_fri(messages: Sequence[bytes], log_n: int, n_layers: int, num_queries
             for k in range(n_layers):
                 m = 1 << (log_n - k)
                 depth = log_n - k
+                extra = None
                 if m == 1:
-                    extra = take()
+                    extra = take()                       # fri_commit.rs:147-149 sends layer[0] first
                     ch.send(extra)
                 i = idx % m
                 sib = (i + m // 2) % m
                 vb, path, sb, spath = take(), take(), take(), take()
+                if extra is not None and extra != vb:
+                    return False
                 for msg in (vb, path, sb, spath):
                     ch.send(msg)
                 v, sv = int.from_bytes(vb, "big"), int.from_bytes(sb, "big")

@@ -1,0 +1,396 @@
+// Tests of the C++ host mirror (stark-prover_amd/host/stark101.hpp), written
+// like the reference's own unit tests:
+//   cpu: src/fields/element.rs:149-290 and src/polynomial/ops.rs:551-990
+//        restated over FieldElement<7>; SHA-256 FIPS 180-4 vectors; the
+//        Channel replayed against every golden transcript; verify_fri on
+//        full oracle transcripts (accept + tamper).
+//   gpu: fri_commit / decommit_fri / MerkleTree / interpolate / batch
+//        inverse through libfri_amd.so against tests/golden (bit-exact).
+// Usage: test_stark101 [cpu|gpu|all]; exit status = number of failures.
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "stark101.hpp"
+
+using namespace stark101;
+
+struct GoldenCase {
+    const char* name;
+    uint32_t log_n;
+    uint64_t offset;
+    std::vector<uint32_t> coeffs;
+    const char* channel_in;
+    bool forced;
+    std::vector<const char*> roots;
+    std::vector<uint32_t> betas;
+    uint64_t final_value;
+    int final_degree;
+    const char* channel_out;
+    size_t proof_size;
+    const char* dq3_state;
+    size_t dq3_messages;
+    const char* dq3_sha;
+};
+struct GoldenTranscript {
+    const char* name;
+    uint32_t log_n;
+    size_t n_layers, num_queries, max_index;
+    uint64_t offset;
+    const char* channel_in;
+    std::vector<const char*> messages_hex;
+};
+#include "golden_cases.inc"
+
+// ------------------------------------------------------------ tiny harness
+struct Failure {
+    std::string msg;
+};
+#define ASSERT_TRUE(c)                                                                               \
+    do {                                                                                             \
+        if (!(c)) throw Failure{std::string(__FILE__ ":") + std::to_string(__LINE__) + ": " #c};     \
+    } while (0)
+#define ASSERT_EQ(a, b)                                                                              \
+    do {                                                                                             \
+        if (!((a) == (b))) throw Failure{std::string(__FILE__ ":") + std::to_string(__LINE__) + ": " #a " != " #b}; \
+    } while (0)
+#define ASSERT_PANICS(stmt)                                                                          \
+    do {                                                                                             \
+        bool _p = false;                                                                             \
+        try { stmt; } catch (const Panic&) { _p = true; }                                            \
+        if (!_p) throw Failure{std::string(__FILE__ ":") + std::to_string(__LINE__) + ": no panic: " #stmt}; \
+    } while (0)
+
+struct Test {
+    const char* group;
+    const char* name;
+    std::function<void()> fn;
+};
+static std::vector<Test>& registry() {
+    static std::vector<Test> r;
+    return r;
+}
+struct Reg {
+    Reg(const char* g, const char* n, std::function<void()> f) { registry().push_back({g, n, std::move(f)}); }
+};
+#define TEST(group, name)                                   \
+    static void group##_##name();                           \
+    static Reg reg_##group##_##name(#group, #name, group##_##name); \
+    static void group##_##name()
+
+using F7 = FieldElement<7>;
+using P7 = Polynomial<7>;
+
+static std::vector<uint8_t> bytes_of(const char* hex) { return sha::from_hex(hex); }
+static std::vector<uint8_t> str_bytes(const std::string& s) { return std::vector<uint8_t>(s.begin(), s.end()); }
+
+// ============================================== element.rs:149-290 (mod 7)
+TEST(cpu, test_field_add) { ASSERT_EQ((F7(1) + F7(2)).value(), 3u); }
+TEST(cpu, test_field_sub) { ASSERT_EQ((F7(1) - F7(2)).value(), 6u); }
+TEST(cpu, test_field_mul) { ASSERT_EQ((F7(3) * F7(4)).value(), 5u); }
+TEST(cpu, test_field_div) { ASSERT_EQ((F7(1) / F7(3)).value(), 5u); }
+TEST(cpu, test_field_inverse) { ASSERT_EQ(F7(3).inverse().value(), 5u); }
+TEST(cpu, test_field_pow) { ASSERT_EQ(F7(3).pow(3).value(), 6u); }
+TEST(cpu, test_zero_and_one) {
+    ASSERT_EQ(F7::zero().value(), 0u);
+    ASSERT_EQ(F7::one().value(), 1u);
+}
+TEST(cpu, test_negation) { ASSERT_EQ((-F7(3)).value(), 4u); }
+TEST(cpu, test_random_generation) {
+    for (int i = 0; i < 100; i++) ASSERT_TRUE(F7::random().value() < 7);
+}
+TEST(cpu, test_modular_wraparound) { ASSERT_EQ((F7(10) + F7(12)).value(), 1u); }
+TEST(cpu, test_equality) { ASSERT_TRUE(F7(3) == F7(10)); }
+TEST(cpu, test_field_add_assign) {
+    F7 a(3);
+    a += F7(5);
+    ASSERT_EQ(a.value(), 1u);
+}
+TEST(cpu, test_field_sub_assign) {
+    F7 a(3);
+    a -= F7(5);
+    ASSERT_EQ(a.value(), 5u);
+}
+TEST(cpu, test_field_mul_assign) {
+    F7 a(3);
+    a *= F7(5);
+    ASSERT_EQ(a.value(), 1u);
+}
+TEST(cpu, test_field_div_assign) {
+    F7 a(3);
+    a /= F7(5);
+    ASSERT_EQ(a.value(), 2u);
+}
+TEST(cpu, test_pow_zero) { ASSERT_EQ(F7(3).pow(0).value(), 1u); }
+TEST(cpu, test_pow_one) { ASSERT_EQ(F7(3).pow(1).value(), 3u); }
+TEST(cpu, test_inverse_multiplication) { ASSERT_EQ((F7(3) * F7(3).inverse()).value(), 1u); }
+// frozen-field extras: inverse(0) = 0 (Fermat), From<i128>, to_bytes big endian
+TEST(cpu, frozen_field_edges) {
+    ASSERT_EQ(FE(0).inverse().value(), 0u);
+    ASSERT_EQ(FE::from_i128(-1).value(), P - 1);
+    ASSERT_EQ((FE(P - 1) * FE(P - 1)).value(), 1u);
+    auto b = FE(0x01020304u).to_bytes();
+    const uint8_t want[8] = {0, 0, 0, 0, 1, 2, 3, 4};
+    ASSERT_TRUE(std::memcmp(b.data(), want, 8) == 0);
+    for (uint32_t l = 1; l <= 30; l++) {
+        ASSERT_EQ(omega(l).pow(uint64_t{1} << l).value(), 1u);
+        ASSERT_EQ(omega(l).pow(uint64_t{1} << (l - 1)).value(), P - 1);
+    }
+    ASSERT_PANICS(omega(31));
+}
+
+// ================================================ ops.rs:551-990 (mod 7)
+TEST(cpu, test_zero_polynomial) {
+    P7 p = P7::zero();
+    ASSERT_EQ(p.degree, -1);
+    ASSERT_TRUE(p.is_zero());
+}
+TEST(cpu, test_evaluate_zero_polynomial) { ASSERT_TRUE(P7::zero().evaluate(F7::zero()) == F7::zero()); }
+TEST(cpu, test_evaluate_constant_polynomial) { ASSERT_TRUE(P7({F7(5)}).evaluate(F7::zero()) == F7(5)); }
+TEST(cpu, test_create_with_empty_coeffs) {
+    P7 p(std::vector<F7>{});
+    ASSERT_TRUE(p.is_zero());
+    ASSERT_EQ(p.coefficients.size(), 0u);
+    ASSERT_EQ(p.degree, -1);
+}
+TEST(cpu, test_create_with_trailing_zeros) {
+    P7 p({F7(1), F7(2), F7::zero(), F7::zero()});
+    ASSERT_EQ(p.degree, 1);
+    ASSERT_EQ(p.coefficients.size(), 2u);
+    ASSERT_TRUE(p.coefficients[0] == F7(1));
+    ASSERT_TRUE(p.coefficients[1] == F7(2));
+}
+TEST(cpu, test_is_zero) {
+    ASSERT_TRUE(P7::zero().is_zero());
+    ASSERT_TRUE(!P7({F7(0), F7(1)}).is_zero());
+}
+TEST(cpu, test_leading_coefficient) {
+    ASSERT_TRUE(*P7({F7(2), F7(5)}).leading_coefficient() == F7(5));
+    ASSERT_TRUE(!P7::zero().leading_coefficient().has_value());
+}
+TEST(cpu, test_partial_eq_diff_length) { ASSERT_TRUE(P7({F7(1), F7(2)}) != P7({F7(1), F7(2), F7(3)})); }
+TEST(cpu, test_partial_eq_diff_coeff) { ASSERT_TRUE(P7({F7(1), F7(2)}) != P7({F7(1), F7(3)})); }
+TEST(cpu, horner_matches_powers) {
+    Poly p({FE(3), FE(0), FE(P - 1), FE(12345)});
+    FE x(987654321);
+    ASSERT_TRUE(p.evaluate(x) == FE(3) + FE(P - 1) * x.pow(2) + FE(12345) * x.pow(3));
+}
+TEST(cpu, coset_domain) {
+    Coset c(FE(5), omega(4), 16);
+    auto d = c.generate_coset_domain();
+    ASSERT_EQ(d.size(), 16u);
+    ASSERT_TRUE(d[0] == FE(5));
+    ASSERT_TRUE(d[3] == FE(5) * omega(4).pow(3));
+    ASSERT_TRUE(d[8] == -d[0]);                         // -D[i] = D[i + n/2]
+}
+
+// ======================================================== SHA-256 / channel
+TEST(cpu, sha256_fips_vectors) {
+    ASSERT_EQ(sha::digest_hex(""), std::string("e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"));
+    ASSERT_EQ(sha::digest_hex("abc"), std::string("ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"));
+    ASSERT_EQ(sha::digest_hex("abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq"),
+              std::string("248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"));
+    std::string a(1000, 'a');
+    ASSERT_EQ(sha::digest_hex(a), std::string("41edece42d63e8d9bf515a9ba6932e1c20cbc9f5a5d134645adb5db1b9737ea3"));
+}
+TEST(cpu, channel_send_and_draw) {
+    FriChannel ch;
+    ASSERT_PANICS(ch.receive_random_int(0, 10, false));  // channel.rs:65: "" is not valid hex
+    const uint8_t m[3] = {0xde, 0xad, 0x01};
+    ch.send(m, 3);
+    ASSERT_EQ(ch.state, sha::digest_hex("dead01"));
+    const std::string s0 = ch.state;
+    FE beta = ch.receive_random_field_element();
+    ASSERT_EQ(ch.state, sha::digest_hex(s0));
+    ASSERT_EQ(ch.proof.size(), 2u);
+    ASSERT_EQ(ch.compressed_proof.size(), 1u);
+    ASSERT_TRUE(ch.proof[1] == FriChannel::be64(beta.value()));
+    ASSERT_EQ(ch.proof_size(), 11u);
+    ASSERT_EQ(ch.compressed_proof_size(), 3u);
+    // channel.rs:70-73: num = (state + min) % (max - min + 1) is NOT shifted
+    // by min, so a one-value range [5, 5] yields 0 (reference quirk kept).
+    uint64_t r = ch.receive_random_int(5, 5, true);
+    ASSERT_EQ(r, 0u);
+    ASSERT_EQ(ch.proof.size(), 3u);
+}
+// The host Channel replays every golden commit transcript: roots sent as
+// hex ASCII, betas drawn, final value sent (fri_commit.rs:84-114).
+TEST(cpu, channel_replays_golden_commits) {
+    for (const auto& c : GOLDEN) {
+        if (c.forced) continue;
+        FriChannel ch;
+        ch.state = c.channel_in;
+        for (size_t k = 0; k < c.roots.size(); k++) {
+            ch.send(str_bytes(c.roots[k]));
+            if (k < c.betas.size()) ASSERT_EQ(ch.receive_random_field_element().value(), c.betas[k]);
+        }
+        ch.send(FE(c.final_value).to_bytes());
+        ASSERT_EQ(ch.state, std::string(c.channel_out));
+        ASSERT_EQ(ch.proof_size(), c.proof_size);
+    }
+}
+
+// ======================================================= verify_fri (host)
+static std::vector<std::vector<uint8_t>> messages(const GoldenTranscript& t) {
+    std::vector<std::vector<uint8_t>> m;
+    for (auto* h : t.messages_hex) m.push_back(bytes_of(h));
+    return m;
+}
+TEST(cpu, verify_fri_accepts_golden_transcripts) {
+    for (const auto& t : TRANSCRIPTS)
+        ASSERT_TRUE(verify_fri(messages(t), t.log_n, t.n_layers, t.num_queries, t.max_index, FE(t.offset), t.channel_in));
+}
+TEST(cpu, verify_fri_rejects_tampering) {
+    for (const auto& t : TRANSCRIPTS) {
+        auto good = messages(t);
+        auto ok = [&](const std::vector<std::vector<uint8_t>>& m, size_t nl = 0, uint64_t off = 0) {
+            return verify_fri(m, t.log_n, nl ? nl : t.n_layers, t.num_queries, t.max_index, FE(off ? off : t.offset),
+                              t.channel_in);
+        };
+        for (size_t i = 0; i < good.size(); i++) {
+            if (good[i].empty()) continue;
+            auto bad = good;
+            bad[i][bad[i].size() / 2] ^= 0x01;
+            ASSERT_TRUE(!ok(bad));
+        }
+        auto trunc = good;
+        trunc.pop_back();
+        ASSERT_TRUE(!ok(trunc));
+        auto extra = good;
+        extra.push_back({0});
+        ASSERT_TRUE(!ok(extra));
+        ASSERT_TRUE(!ok(good, t.n_layers + 1));
+        ASSERT_TRUE(!ok(good, 0, 7));
+        ASSERT_TRUE(!verify_fri(good, t.log_n, t.n_layers, t.num_queries, t.max_index, FE(t.offset), "00"));
+    }
+}
+
+// ================================================================== GPU
+static Coset coset_of(const GoldenCase& c) { return Coset(FE(c.offset), omega(c.log_n), size_t{1} << c.log_n); }
+static Poly poly_of(const GoldenCase& c) {
+    std::vector<FE> v;
+    for (auto x : c.coeffs) v.push_back(FE(x));
+    return Poly(v);
+}
+static std::string transcript_sha(const std::vector<std::vector<uint8_t>>& proof, size_t from) {
+    std::vector<uint8_t> buf;
+    for (size_t i = from; i < proof.size(); i++) {
+        const uint32_t n = static_cast<uint32_t>(proof[i].size());
+        for (int b = 0; b < 4; b++) buf.push_back(static_cast<uint8_t>(n >> (8 * b)));
+        buf.insert(buf.end(), proof[i].begin(), proof[i].end());
+    }
+    auto d = sha::digest(buf.data(), buf.size());
+    return sha::hex(d.data(), 32);
+}
+
+TEST(gpu, fri_commit_and_decommit_match_golden) {
+    int checked = 0;
+    for (const auto& c : GOLDEN) {
+        if (c.forced) continue;                          // no forced-beta hook in the reference API
+        FriChannel ch;
+        ch.state = c.channel_in;
+        FRIProof proof = fri_commit(poly_of(c), coset_of(c).generate_coset_domain(), ch);
+        ASSERT_EQ(proof.n_layers(), c.roots.size());
+        for (size_t k = 0; k < c.roots.size(); k++) ASSERT_EQ(proof.fri_merkles[k].root(), std::string(c.roots[k]));
+        ASSERT_EQ(proof.betas.size(), c.betas.size());
+        for (size_t k = 0; k < c.betas.size(); k++) ASSERT_EQ(proof.betas[k].value(), c.betas[k]);
+        if (c.final_degree < 0) {
+            ASSERT_TRUE(proof.final_poly.is_zero());
+        } else {
+            ASSERT_EQ(proof.final_poly.degree, 0);
+            ASSERT_EQ(proof.final_poly.coefficients[0].value(), c.final_value);
+        }
+        ASSERT_EQ(ch.state, std::string(c.channel_out));
+        ASSERT_EQ(ch.proof_size(), c.proof_size);
+        const size_t n_commit = ch.proof.size();
+        const size_t max_index = (size_t{1} << c.log_n) - 1;
+        decommit_fri(3, max_index, proof, ch);
+        ASSERT_EQ(ch.state, std::string(c.dq3_state));
+        ASSERT_EQ(ch.proof.size() - n_commit, c.dq3_messages);
+        ASSERT_EQ(transcript_sha(ch.proof, n_commit), std::string(c.dq3_sha));
+        ASSERT_TRUE(verify_fri(ch.proof, c.log_n, proof.n_layers(), 3, max_index, FE(c.offset), c.channel_in));
+        checked++;
+    }
+    ASSERT_TRUE(checked >= 30);
+}
+TEST(gpu, layers_lde_interpolate_merkle) {
+    const GoldenCase* c = nullptr;
+    for (const auto& g : GOLDEN)
+        if (std::string(g.name) == "rand_n10_s42") c = &g;
+    ASSERT_TRUE(c != nullptr);
+    Poly p = poly_of(*c);
+    Coset co = coset_of(*c);
+    FriChannel ch;
+    FRIProof proof = fri_commit(p, co, ch);
+    auto layers = proof.fri_layers();
+    auto lde = evaluate_on_coset(p, co);
+    ASSERT_TRUE(layers[0] == lde);
+    auto dom = co.generate_coset_domain();
+    for (size_t i : {size_t{0}, size_t{1}, size_t{517}, size_t{1023}}) ASSERT_TRUE(lde[i] == p.evaluate(dom[i]));
+    ASSERT_TRUE(interpolate(dom, lde) == p);
+    for (size_t k = 0; k < layers.size(); k++) ASSERT_EQ(MerkleTree(layers[k]).root(), proof.fri_merkles[k].root());
+    // the last layer is the final constant everywhere
+    for (auto v : layers.back()) ASSERT_TRUE(v == proof.final_poly.coefficients[0]);
+    // auth path of a committed tree leads to its root
+    auto path = proof.fri_merkles[0].get_authentication_path(5);
+    ASSERT_EQ(path.size(), 32u * c->log_n);
+    ASSERT_PANICS(MerkleTree(layers[1]).get_authentication_path(0));
+    // a later commit on the same Gpu retires this proof's layers
+    FriChannel ch2;
+    fri_commit(p, co, ch2);
+    ASSERT_TRUE(!proof.resident());
+    ASSERT_PANICS(proof.fri_layer(0));
+    ASSERT_PANICS(proof.fri_merkles[0].get_authentication_path(0));
+    FriChannel ch3;
+    ASSERT_PANICS(decommit_fri(1, 7, proof, ch3));
+}
+TEST(gpu, batch_inverse_matches_fermat) {
+    std::vector<FE> xs;
+    for (uint64_t i = 0; i < 5000; i++) xs.push_back(FE(i * 2654435761u + (i % 7 == 0 ? 0 : 1)));
+    xs[0] = FE(0);
+    xs[1] = FE(P - 1);
+    auto inv = batch_inverse(xs);
+    ASSERT_EQ(inv.size(), xs.size());
+    for (size_t i = 0; i < xs.size(); i++) ASSERT_TRUE(inv[i] == xs[i].inverse());
+}
+TEST(gpu, reference_panics) {
+    const auto& c = GOLDEN[10];
+    auto gpu = Gpu::thread_default(c.log_n);           // outside ASSERT_PANICS: no device is a failure here
+    ASSERT_TRUE(gpu->ctx() != nullptr);
+    auto dom = coset_of(c).generate_coset_domain();
+    FriChannel ch;
+    auto bad = dom;
+    std::swap(bad[1], bad[2]);
+    ASSERT_PANICS(fri_commit(poly_of(c), bad, ch));                        // not offset*<w_n>
+    bad = dom;
+    bad.pop_back();
+    ASSERT_PANICS(fri_commit(poly_of(c), bad, ch));                        // not a power of two
+    std::vector<FE> big(dom.size() + 1, FE(1));
+    ASSERT_PANICS(fri_commit(Poly(big), dom, ch));                         // degree >= n: merkle/mod.rs:25
+    ASSERT_PANICS(interpolate(dom, std::vector<FE>(dom.size() - 1)));      // interpolation.rs:127
+    ASSERT_PANICS(MerkleTree(std::vector<FE>{}));                          // merkle/mod.rs:25
+    ASSERT_EQ(ch.proof.size(), 0u);                                        // nothing sent on failure
+}
+
+int main(int argc, char** argv) {
+    const std::string which = argc > 1 ? argv[1] : "cpu";
+    int fails = 0, ran = 0;
+    for (auto& t : registry()) {
+        if (which != "all" && which != t.group) continue;
+        ran++;
+        try {
+            t.fn();
+            std::printf("ok   %s::%s\n", t.group, t.name);
+        } catch (const Failure& f) {
+            fails++;
+            std::printf("FAIL %s::%s: %s\n", t.group, t.name, f.msg.c_str());
+        } catch (const std::exception& e) {
+            fails++;
+            std::printf("FAIL %s::%s: exception: %s\n", t.group, t.name, e.what());
+        }
+    }
+    std::printf("%d tests, %d failures\n", ran, fails);
+    return fails;
+}

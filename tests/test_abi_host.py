@@ -163,3 +163,20 @@ def test_verify_fri_rejects_tampering(oracle):
     assert not fri_amd.verify_fri(msgs[:-1], *args)            # truncated
     assert not fri_amd.verify_fri(msgs + [b"x"], *args)        # trailing garbage
     assert not fri_amd.verify_fri(msgs, log_n, n_layers, 4, (1 << log_n) - 2)   # other query indices
+
+
+def test_verify_fri_rejects_every_flipped_message_blowup1(oracle):
+    """Blowup 1 ends in a 1-element layer, whose value the reference sends
+    twice (fri_commit.rs:147-149).  The first copy of the last query feeds
+    nothing downstream, so the verifier must compare it with the value."""
+    import fri_amd
+    log_n = 5
+    msgs, n_layers = _oracle_transcript(oracle, oracle.splitmix64_field(6, 32), log_n, 3)
+    args = (log_n, n_layers, 3, (1 << log_n) - 1)
+    assert fri_amd.verify_fri(msgs, *args)
+    for i, m in enumerate(msgs):
+        if not m:
+            continue
+        b = bytearray(m)
+        b[len(b) // 2] ^= 1
+        assert not fri_amd.verify_fri(msgs[:i] + [bytes(b)] + msgs[i + 1:], *args), i

@@ -1,0 +1,59 @@
+"""Runs the C++ host-mirror tests (tests/cpp/test_stark101.cpp) — the
+reference-shaped C++ API (stark-prover_amd/host/stark101.hpp) over
+libfri_amd.so.  The CPU group needs no device; the GPU group drives the
+device through the C ABI and compares with tests/golden bit for bit."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "stark-prover_amd")
+BIN = os.path.join(PKG, "build", "test_stark101")
+
+
+def _build():
+    subprocess.run(["make", "-s", "-C", PKG, "test_host"], check=True, timeout=600)
+
+
+def _run(group):
+    _build()
+    p = subprocess.run([BIN, group], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-4000:] + p.stderr[-2000:]
+    assert " 0 failures" in p.stdout
+    return p.stdout
+
+
+def test_golden_include_is_current():
+    """golden_cases.inc is generated from fri_golden.json; it must not drift."""
+    import json
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "fri_golden.json")))
+    inc = open(os.path.join(ROOT, "tests", "cpp", "golden_cases.inc")).read()
+    for c in g["cases"]:
+        assert f'"{c["name"]}"' in inc and f'"{c["channel_out"]}"' in inc, c["name"]
+
+
+def test_cpp_host_mirror_cpu():
+    out = _run("cpu")
+    assert "ok   cpu::channel_replays_golden_commits" in out
+    assert "ok   cpu::verify_fri_rejects_tampering" in out
+
+
+def test_host_library_exports_reference_api():
+    _build()
+    syms = subprocess.run(["nm", "-DC", "--defined-only", os.path.join(PKG, "lib", "libstark101.so")],
+                          capture_output=True, text=True, check=True).stdout
+    for name in ("stark101::fri_commit(", "stark101::decommit_fri(", "stark101::decommit_fri_layers(",
+                 "stark101::verify_fri(", "stark101::MerkleTree::MerkleTree(", "stark101::interpolate(",
+                 "stark101::batch_inverse(", "stark101::evaluate_on_coset("):
+        assert name in syms, name
+    needed = subprocess.run(["readelf", "-d", os.path.join(PKG, "lib", "libstark101.so")],
+                            capture_output=True, text=True, check=True).stdout
+    assert "libfri_amd.so" in needed                      # the device path, no CPU fallback
+    assert "oracle" not in needed
+
+
+@pytest.mark.gpu
+def test_cpp_host_mirror_gpu():
+    out = _run("gpu")
+    assert "ok   gpu::fri_commit_and_decommit_match_golden" in out
