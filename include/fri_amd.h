@@ -138,6 +138,31 @@ int fri_trace_commit(fri_ctx* ctx, const uint32_t* trace, uint32_t log_t, uint32
                      uint32_t offset, uint8_t root32[32], uint32_t* coeffs_out, size_t* coeff_len,
                      uint32_t* lde_out);
 
+/* Prover slice (BASELINE configs[3]; src/prover, src/composition are empty in
+ * the reference, so the constraint system is STARK-101's FibonacciSq — the
+ * crate is `stark-101`, Cargo.toml:2 — on the full trace subgroup G = <g>,
+ * |G| = T = 2^log_t):  a_0 = 1, a_{T-1} = a_last, a_{i+2} = a_{i+1}^2 + a_i^2.
+ * From the trace LDE kept by the last fri_trace_commit (same log_t,
+ * log_blowup, offset) computes, on the coset offset*<w_n>,
+ *   CP = alphas[0] (f-1)/(x-1) + alphas[1] (f-a_last)/(x-g^{T-1})
+ *      + alphas[2] (f(g^2 x) - f(g x)^2 - f^2) (x-g^{T-2})(x-g^{T-1}) / (x^T-1)
+ * (two divisions per point through one batch inversion), interpolates it and
+ * runs fri_commit on it: the FRI of fri_commit.rs:72-122 over the composition
+ * polynomial, channel continued from chan_in (after the trace root and the
+ * three alphas were drawn).  FRI_EDEGREE if deg CP > T (trace violates the
+ * constraints).  log_blowup 1..4.  Layers stay resident for fri_decommit_query. */
+int fri_fibsq_composition_commit(fri_ctx* ctx, uint32_t log_t, uint32_t log_blowup, uint32_t offset,
+                                 uint32_t a_last, const uint32_t alphas[3],
+                                 const fri_channel_state* chan_in, uint32_t flags,
+                                 fri_commit_result* out);
+
+/* Trace-tree decommitment (STARK-101 decommit_on_query: f(x), f(gx), f(g^2x)
+ * with their paths): values[j] = LDE[(index + j*stride) mod n], j < count
+ * (1..8); paths = count authentication paths of log2(n) sibling digests
+ * (leaf -> root, 32 bytes each), as fri_auth_path formats them. */
+int fri_trace_decommit(fri_ctx* ctx, uint64_t index, uint64_t stride, uint32_t count, uint32_t* values,
+                       uint8_t* paths, size_t paths_cap);
+
 /* ---------------------------------------------------------- FRI commit */
 /* Full FRI commit — fri_commit(poly, domain, &mut channel)
  * (src/fri/fri_commit.rs:72-122): LDE of `coeffs` on offset*<w_n>,

@@ -625,6 +625,98 @@ int orc_fri_commit_fast(const uint64_t* coeffs, size_t d, uint32_t log_n, uint64
     return 0;
 }
 
+/* ======================================================================
+ * C.   Prover slice — STARK-101 FibonacciSq (BASELINE configs[3]).
+ *      The reference's src/prover, src/trace, src/composition are EMPTY;
+ *      restated from the STARK-101 tutorial on the full trace subgroup
+ *      G = <g>, |G| = T (PARITY UNPINNED; the Python twin's
+ *      fibsq_cp_faithful builds the same polynomial with the reference's
+ *      div_rem / mul / compose, ops.rs:114-237).
+ *      CP = a0 (f-1)/(x-1) + a1 (f-A)/(x-g^{T-1})
+ *         + a2 (f(g^2x) - f(gx)^2 - f^2)(x-g^{T-2})(x-g^{T-1})/(x^T-1)
+ * ====================================================================== */
+void orc_fibsq_trace(uint64_t a1, size_t T, uint64_t M, uint64_t* out) {
+    for (size_t i = 0; i < T; i++)
+        out[i] = i == 0 ? 1 : i == 1 ? a1 % M
+                 : orc_fe_add(orc_fe_mul(out[i - 1], out[i - 1], M), orc_fe_mul(out[i - 2], out[i - 2], M), M);
+}
+
+/* f: LDE of the trace polynomial on offset*<w_n>, n = 2^(log_t+log_b). */
+int orc_fibsq_cp_evals(const uint64_t* f, uint32_t log_t, uint32_t log_b, uint64_t offset, uint64_t gen,
+                       uint64_t M, uint64_t a_last, const uint64_t* alphas, uint64_t* out) {
+    const uint32_t L = log_t + log_b;
+    const size_t n = (size_t)1 << L, T = (size_t)1 << log_t, B = (size_t)1 << log_b;
+    const uint64_t w = orc_fe_pow(gen, (M - 1) >> L, M), g = orc_fe_pow(gen, (M - 1) >> log_t, M);
+    const uint64_t glast = orc_fe_pow(g, T - 1, M), gprev = orc_fe_pow(g, T - 2, M);
+    uint64_t* x = (uint64_t*)malloc(n * sizeof(uint64_t));
+    uint64_t* den = (uint64_t*)malloc(2 * n * sizeof(uint64_t));
+    uint64_t* dinv = (uint64_t*)malloc(2 * n * sizeof(uint64_t));
+    if (!x || !den || !dinv) { free(x); free(den); free(dinv); return -1; }
+    uint64_t xv = offset;
+    for (size_t i = 0; i < n; i++) { x[i] = xv; xv = orc_fe_mul(xv, w, M); }
+    for (size_t i = 0; i < n; i++) {
+        den[i] = orc_fe_sub(x[i], 1, M);                                   /* x - 1        */
+        den[n + i] = orc_fe_sub(x[i], glast, M);                           /* x - g^{T-1}  */
+    }
+    orc_batch_inverse(den, dinv, 2 * n, M);
+    uint64_t zinv[64];                      /* x^T depends on i mod B only */
+    for (size_t j = 0; j < B && j < 64; j++) zinv[j] = orc_fe_inverse(orc_fe_sub(orc_fe_pow(x[j], T, M), 1, M), M);
+    #pragma omp parallel for schedule(static) if (n >= 1 << 14)
+    for (long li = 0; li < (long)n; li++) {
+        size_t i = (size_t)li;
+        uint64_t f0 = f[i], f1 = f[(i + B) % n], f2 = f[(i + 2 * B) % n];
+        uint64_t p0 = orc_fe_mul(orc_fe_sub(f0, 1, M), dinv[i], M);
+        uint64_t p1 = orc_fe_mul(orc_fe_sub(f0, a_last, M), dinv[n + i], M);
+        uint64_t num = orc_fe_sub(f2, orc_fe_add(orc_fe_mul(f1, f1, M), orc_fe_mul(f0, f0, M), M), M);
+        uint64_t zf = orc_fe_mul(orc_fe_mul(orc_fe_sub(x[i], gprev, M), orc_fe_sub(x[i], glast, M), M),
+                                 zinv[i % B], M);
+        uint64_t p2 = orc_fe_mul(num, zf, M);
+        out[i] = orc_fe_add(orc_fe_add(orc_fe_mul(p0, alphas[0], M), orc_fe_mul(p1, alphas[1], M), M),
+                            orc_fe_mul(p2, alphas[2], M), M);
+    }
+    free(x); free(den); free(dinv);
+    return 0;
+}
+
+/* Commit phase of the prover (no queries): trace -> interpolate on G ->
+ * LDE -> Merkle -> send(root hex) -> alpha_0..2 -> CP evals -> coefficients
+ * -> orc_fri_commit_fast.  Optional outputs as orc_fri_commit_fast, plus the
+ * trace LDE (n values) and its tree (orc_merkle_build layout). */
+int orc_fibsq_prove_commit(uint64_t a1, uint32_t log_t, uint32_t log_b, uint64_t offset, uint64_t gen, uint64_t M,
+                           orc_channel* ch, uint8_t trace_root[32], uint64_t alphas[3], orc_fri_result* res,
+                           uint64_t* f_eval_out, uint8_t* f_tree_out, uint64_t* layers_out, uint8_t* trees_out) {
+    const uint32_t L = log_t + log_b;
+    const size_t n = (size_t)1 << L, T = (size_t)1 << log_t;
+    uint64_t* tr = (uint64_t*)malloc(T * sizeof(uint64_t));
+    uint64_t* fc = (uint64_t*)malloc(T * sizeof(uint64_t));
+    uint64_t* fe = (uint64_t*)malloc(n * sizeof(uint64_t));
+    uint64_t* cp = (uint64_t*)malloc(n * sizeof(uint64_t));
+    uint64_t* cc = (uint64_t*)malloc(n * sizeof(uint64_t));
+    size_t cnt = orc_merkle_nodes_count(n);
+    uint8_t* nodes = (uint8_t*)malloc(32 * cnt);
+    int rc = -1;
+    if (!tr || !fc || !fe || !cp || !cc || !nodes) goto out;
+    orc_fibsq_trace(a1, T, M, tr);
+    {
+        size_t fl = orc_interpolate_coset(tr, log_t, 1, gen, M, fc);
+        if (orc_lde(fc, fl, L, offset, gen, M, fe)) goto out;
+    }
+    orc_merkle_build(fe, n, nodes);
+    memcpy(trace_root, nodes + 32 * (cnt - 1), 32);
+    send_root(ch, trace_root);
+    for (int j = 0; j < 3; j++) alphas[j] = orc_channel_receive_fe(ch, M);
+    if (orc_fibsq_cp_evals(fe, log_t, log_b, offset, gen, M, tr[T - 1], alphas, cp)) goto out;
+    {
+        size_t cl = orc_interpolate_coset(cp, L, offset, gen, M, cc);
+        rc = orc_fri_commit_fast(cc, cl, L, offset, gen, M, ch, NULL, res, layers_out, trees_out);
+    }
+    if (f_eval_out) memcpy(f_eval_out, fe, n * sizeof(uint64_t));
+    if (f_tree_out) memcpy(f_tree_out, nodes, 32 * cnt);
+out:
+    free(tr); free(fc); free(fe); free(cp); free(cc); free(nodes);
+    return rc;
+}
+
 void orc_set_num_threads(int n) {
 #ifdef _OPENMP
     omp_set_num_threads(n);

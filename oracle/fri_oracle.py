@@ -369,6 +369,138 @@ def decommit_fri(num_queries: int, max_index: int, layers, trees, channel: Chann
         decommit_fri_layers(idx, layers, trees, channel)
 
 
+# --------------------------------------------------------------------------
+# Prover slice — STARK-101 FibonacciSq (BASELINE configs[3]).  The
+# reference's src/prover, src/trace, src/composition are EMPTY files, so this
+# restates the STARK-101 tutorial's prover (the crate is `stark-101`,
+# Cargo.toml:2) on the full trace subgroup G = <g>, |G| = T, with the
+# reference's own polynomial operations (ops.rs add/sub/mul/div_rem/compose,
+# interpolation.rs Lagrange, Horner evaluate) — PARITY UNPINNED (no reference
+# prover exists to compare with).
+# --------------------------------------------------------------------------
+
+def fibsq_trace(a1: int, T: int, M: int = P) -> List[int]:
+    """a_0 = 1, a_1 = a1, a_{i+2} = a_{i+1}^2 + a_i^2."""
+    a = [1, a1 % M]
+    while len(a) < T:
+        a.append(fe_add(fe_mul(a[-1], a[-1], M), fe_mul(a[-2], a[-2], M), M))
+    return a[:T]
+
+
+def fibsq_cp_faithful(f: List[int], log_t: int, a_last: int, alphas: Sequence[int], M: int = P) -> List[int]:
+    """Composition polynomial in coefficient form, STARK-101 part 2, with the
+    reference's polynomial arithmetic:
+      p0 = (f - 1) / (x - 1),  p1 = (f - A) / (x - g^{T-1}),
+      p2 = (f(g^2 x) - f(g x)^2 - f^2) / ((x^T - 1) / ((x - g^{T-2})(x - g^{T-1}))),
+      CP = a0 p0 + a1 p1 + a2 p2.   Every division must be exact."""
+    T = 1 << log_t
+    g = fe_pow(GEN, (M - 1) >> log_t, M)
+    glast, gprev = fe_pow(g, T - 1, M), fe_pow(g, T - 2, M)
+    x_minus = lambda c: poly_trim([fe_neg(c, M), 1])             # noqa: E731
+    p0, r0 = poly_div_rem(poly_sub(f, [1], M), x_minus(1), M)
+    p1, r1 = poly_div_rem(poly_sub(f, poly_trim([a_last]), M), x_minus(glast), M)
+    f1 = poly_compose(f, [0, g], M)                              # f(g x)     (ops.rs:214-237)
+    f2 = poly_compose(f, [0, fe_mul(g, g, M)], M)                # f(g^2 x)
+    num = poly_sub(poly_sub(f2, poly_mul(f1, f1, M), M), poly_mul(f, f, M), M)
+    xT1 = [fe_neg(1, M)] + [0] * (T - 1) + [1]
+    z, rz = poly_div_rem(xT1, poly_mul(x_minus(gprev), x_minus(glast), M), M)
+    p2, r2 = poly_div_rem(num, z, M)
+    if r0 or r1 or rz or r2:
+        raise ValueError("trace violates the constraints (non-exact division)")
+    cp: List[int] = []
+    for a, pk in zip(alphas, (p0, p1, p2)):
+        term = poly_trim(poly_scalar_mul(pk, a, M))
+        if term:
+            cp = poly_add(cp, term, M) if cp else term
+    return cp
+
+
+@dataclass
+class FibsqProof:
+    trace_root: bytes
+    alphas: List[int]
+    fri: FriResult
+    queries: List[int]
+
+
+def fibsq_prove(a1: int, log_t: int, log_blowup: int, num_queries: int, channel: Channel,
+                offset: int = GEN, M: int = P) -> FibsqProof:
+    """STARK-101 prover, faithful algorithms (small T only: O(T^2)):
+    Lagrange interpolation of the trace on G, Horner LDE on offset*<w_n>,
+    rs_merkle tree, send(root), alpha_0..2, composition polynomial,
+    fri_commit (fri_commit.rs:72-122), then per query
+    idx = receive_random_int(0, n - 2B - 1, true): f(x), path, f(gx), path,
+    f(g^2 x), path (STARK-101 decommit_on_query) and decommit_fri_layers."""
+    T, B = 1 << log_t, 1 << log_blowup
+    L = log_t + log_blowup
+    n = 1 << L
+    trace = fibsq_trace(a1, T, M)
+    f = interpolate_lagrange_polynomials(coset_domain(log_t, offset=1, M=M), trace, M)
+    f_eval = [poly_evaluate(f, x, M) for x in coset_domain(L, offset, M=M)]
+    f_levels = merkle_levels(f_eval)
+    channel.send(f_levels[-1][0].hex().encode())
+    alphas = [channel.receive_random_field_element(M) for _ in range(3)]
+    cp = fibsq_cp_faithful(f, log_t, trace[-1], alphas, M)
+    fri = fri_commit(cp, L, channel, offset, M=M)
+    queries = []
+    for _ in range(num_queries):
+        idx = channel.receive_random_int(0, n - 2 * B - 1, True)
+        queries.append(idx)
+        for j in range(3):
+            channel.send(fe_to_bytes(f_eval[idx + j * B]))
+            channel.send(merkle_proof(f_levels, idx + j * B))
+        decommit_fri_layers(idx, fri.layers, fri.trees, channel)
+    return FibsqProof(f_levels[-1][0], alphas, fri, queries)
+
+
+def fibsq_cp_evals_np(f_eval, log_t: int, log_blowup: int, offset: int, a_last: int, alphas: Sequence[int]):
+    """Composition polynomial on the LDE coset, evaluation form, numpy uint64
+    (p < 2^32: products fit in 64 bits).  Same values as evaluating
+    fibsq_cp_faithful's polynomial on offset*<w_n> (checked by tests)."""
+    import numpy as np
+    T, B = 1 << log_t, 1 << log_blowup
+    L = log_t + log_blowup
+    n = 1 << L
+    Pu = np.uint64(P)
+    f = np.asarray(f_eval, dtype=np.uint64) % Pu
+    w = pow(GEN, (P - 1) >> L, P)
+    g = pow(GEN, (P - 1) >> log_t, P)
+    # x_i = offset * w^i via two-level tables
+    lo = np.array([pow(w, j, P) for j in range(1024)], dtype=np.uint64)
+    hi = np.array([pow(w, 1024 * j, P) * offset % P for j in range((n + 1023) // 1024)], dtype=np.uint64)
+    idx = np.arange(n, dtype=np.uint64)
+    x = lo[idx % 1024] * hi[idx // 1024] % Pu
+
+    def mul(a, b):
+        return a * b % Pu
+
+    def inv(a):
+        r = np.ones_like(a)
+        e, base = P - 2, a.copy()
+        while e:
+            if e & 1:
+                r = mul(r, base)
+            base = mul(base, base)
+            e >>= 1
+        return r
+
+    def sub(a, b):
+        return (a + Pu - (b % Pu)) % Pu
+
+    glast, gprev = np.uint64(pow(g, T - 1, P)), np.uint64(pow(g, T - 2, P))
+    f1 = np.roll(f, -B)
+    f2 = np.roll(f, -2 * B)
+    p0 = mul(sub(f, np.uint64(1)), inv(sub(x, np.uint64(1))))
+    p1 = mul(sub(f, np.uint64(a_last)), inv(sub(x, glast)))
+    num = sub(f2, (mul(f1, f1) + mul(f, f)) % Pu)
+    xT = x.copy()
+    for _ in range(log_t):
+        xT = mul(xT, xT)
+    p2 = mul(mul(num, mul(sub(x, gprev), sub(x, glast))), inv(sub(xT, np.uint64(1))))
+    a0, a1, a2 = (np.uint64(a) for a in alphas)
+    return (mul(p0, a0) + mul(p1, a1) + mul(p2, a2)) % Pu
+
+
 def splitmix64_field(seed: int, count: int, M: int = P) -> List[int]:
     """Synthetic coefficients: splitmix64(seed) % M."""
     mask = (1 << 64) - 1
@@ -454,6 +586,14 @@ def load_c_oracle() -> ctypes.CDLL:
     lib.orc_batch_inverse.argtypes = [p64, p64, sz, u64]
     lib.orc_fold_eval.restype = None
     lib.orc_fold_eval.argtypes = [p64, sz, u64, u64, u64, u64, p64]
+    lib.orc_fibsq_trace.restype = None
+    lib.orc_fibsq_trace.argtypes = [u64, sz, u64, p64]
+    lib.orc_fibsq_cp_evals.restype = ctypes.c_int
+    lib.orc_fibsq_cp_evals.argtypes = [p64, ctypes.c_uint32, ctypes.c_uint32, u64, u64, u64, u64, p64, p64]
+    lib.orc_fibsq_prove_commit.restype = ctypes.c_int
+    lib.orc_fibsq_prove_commit.argtypes = [u64, ctypes.c_uint32, ctypes.c_uint32, u64, u64, u64,
+                                           ctypes.POINTER(OrcChannel), ctypes.c_char_p, p64,
+                                           ctypes.POINTER(OrcFriResult), p64, ctypes.c_char_p, p64, ctypes.c_char_p]
     lib.orc_num_threads.restype = ctypes.c_int
     lib.orc_set_num_threads.argtypes = [ctypes.c_int]
     lib.orc_set_num_threads.restype = None

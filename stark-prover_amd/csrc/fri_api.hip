@@ -102,7 +102,10 @@ struct fri_ctx {
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
     uint32_t* dq_buf = nullptr;     // decommitment gather staging (64 KiB)
     uint32_t* trace_tree = nullptr; // Merkle tree of the last fri_trace_commit LDE
-    size_t trace_tree_cap = 0;      // leaves it can hold
+    uint32_t* trace_lde = nullptr;  // ... and the LDE itself (prover: composition, queries)
+    size_t trace_tree_cap = 0;      // leaves they can hold
+    bool trace_valid = false;       // a trace commit is resident
+    uint32_t trace_log_t = 0, trace_log_b = 0, trace_offset = 0;
 };
 
 #define FRI_HIP(ctx, expr)                                                              \
@@ -228,6 +231,7 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     hipFree(ctx->d_state);
     hipFree(ctx->dq_buf);
     hipFree(ctx->trace_tree);
+    hipFree(ctx->trace_lde);
     if (ctx->h_state) hipHostFree(ctx->h_state);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -379,11 +383,15 @@ extern "C" int fri_trace_commit(fri_ctx* ctx, const uint32_t* trace, uint32_t lo
     const size_t nt = (size_t)1 << log_t, n = (size_t)1 << L;
     if (!check_canonical(trace, nt)) return fail(ctx, FRI_EINVAL, "trace value not canonical (>= p)");
     FRI_HIP(ctx, hipSetDevice(ctx->device));
+    ctx->trace_valid = false;
     if (ctx->trace_tree_cap < n) {
         hipFree(ctx->trace_tree);
+        hipFree(ctx->trace_lde);
         ctx->trace_tree = nullptr;
+        ctx->trace_lde = nullptr;
         ctx->trace_tree_cap = 0;
         FRI_HIP(ctx, hipMalloc(&ctx->trace_tree, (n * 2) * 32));
+        FRI_HIP(ctx, hipMalloc(&ctx->trace_lde, n * 4));
         ctx->trace_tree_cap = n;
     }
     hipStream_t s = ctx->stream;
@@ -401,10 +409,10 @@ extern "C" int fri_trace_commit(fri_ctx* ctx, const uint32_t* trace, uint32_t lo
     launch_pow_table(ctx->pow_lo, ctx->pow_hi, L, offset, 1u, s);
     lp.pre_lo = ctx->pow_lo;
     lp.pre_hi = ctx->pow_hi;
-    launch_ntt(lp, ctx->scratch_b, nt, ctx->scratch_c, s);
+    launch_ntt(lp, ctx->scratch_b, nt, ctx->trace_lde, s);
     // Merkle tree of the LDE, every level kept
     LayerTask t{};
-    t.values = ctx->scratch_c;
+    t.values = ctx->trace_lde;
     t.tree = ctx->trace_tree;
     t.L = L;
     launch_layer(t, s);
@@ -412,9 +420,13 @@ extern "C" int fri_trace_commit(fri_ctx* ctx, const uint32_t* trace, uint32_t lo
     uint32_t w[8];
     FRI_HIP(ctx, hipMemcpyAsync(w, ctx->trace_tree + 8 * level_offset(L, L), 32, hipMemcpyDeviceToHost, s));
     if (coeffs_out) FRI_HIP(ctx, hipMemcpyAsync(coeffs_out, ctx->scratch_b, nt * 4, hipMemcpyDeviceToHost, s));
-    if (lde_out) FRI_HIP(ctx, hipMemcpyAsync(lde_out, ctx->scratch_c, n * 4, hipMemcpyDeviceToHost, s));
+    if (lde_out) FRI_HIP(ctx, hipMemcpyAsync(lde_out, ctx->trace_lde, n * 4, hipMemcpyDeviceToHost, s));
     FRI_HIP(ctx, hipStreamSynchronize(s));
     digest_to_bytes(w, root32);
+    ctx->trace_valid = true;
+    ctx->trace_log_t = log_t;
+    ctx->trace_log_b = log_blowup;
+    ctx->trace_offset = offset;
     if (coeffs_out && coeff_len) {
         size_t len = nt;
         while (len > 0 && coeffs_out[len - 1] == 0) len--;      // Polynomial::new trim (ops.rs:19-37)
@@ -765,6 +777,87 @@ extern "C" int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values
     FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
     memcpy(values, h.data(), 2 * dp.n_layers * 4);
     memcpy(paths, h.data() + 2 * dp.n_layers, (size_t)words * 4);
+    return FRI_OK;
+}
+
+// ------------------------------------------------------------- prover ----
+// STARK-101 FibonacciSq composition + FRI commit of the composition
+// polynomial (fri_prover.hip has the constraint system).  Reads the trace LDE
+// kept by the last fri_trace_commit; CP evaluations -> coset iNTT -> the
+// commit of fri_commit_device (layer 0 re-extends exactly those evaluations).
+extern "C" int fri_fibsq_composition_commit(fri_ctx* ctx, uint32_t log_t, uint32_t log_blowup, uint32_t offset,
+                                            uint32_t a_last, const uint32_t alphas[3],
+                                            const fri_channel_state* chan_in, uint32_t flags,
+                                            fri_commit_result* out) {
+    if (!ctx || !alphas || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    if (!ctx->trace_valid || ctx->trace_log_t != log_t || ctx->trace_log_b != log_blowup ||
+        ctx->trace_offset != offset)
+        return fail(ctx, FRI_ESTATE, "no resident trace commit with this (log_t, log_blowup, offset)");
+    if (log_blowup < 1 || ((uint32_t)1 << log_blowup) > FIBSQ_MAX_B)
+        return fail(ctx, FRI_EINVAL, "log_blowup must be 1..4 (deg CP = T needs n > T)");
+    if (log_t < 2) return fail(ctx, FRI_EINVAL, "trace needs at least 4 rows");
+    if (a_last >= P || alphas[0] >= P || alphas[1] >= P || alphas[2] >= P)
+        return fail(ctx, FRI_EINVAL, "a_last / alphas not canonical");
+    if (flags & FRI_FLAG_FORCE_BETAS) return fail(ctx, FRI_EINVAL, "forced betas are not supported here");
+    const uint32_t L = log_t + log_blowup;
+    const size_t n = (size_t)1 << L, T = (size_t)1 << log_t;
+    const uint32_t B = 1u << log_blowup;
+    FibsqParams q{};
+    q.log_n = L;
+    q.B = B;
+    q.offset_m = to_mont(offset);
+    const uint32_t w = root_of_unity(L), g = root_of_unity(log_t), wB = root_of_unity(log_blowup);
+    q.w_m = to_mont(w);
+    q.winv_m = to_mont(inv_std(w));
+    q.glast_m = to_mont(pow_std(g, T - 1));
+    q.gprev_m = to_mont(pow_std(g, T - 2));
+    q.a_last = a_last;
+    for (int j = 0; j < 3; j++) q.alpha_m[j] = to_mont(alphas[j]);
+    const uint32_t offT = pow_std(offset, T);
+    for (uint32_t j = 0; j < B; j++) {
+        const uint32_t z = sub(mul_std(offT, pow_std(wB, j)), 1u);
+        if (z == 0) return fail(ctx, FRI_EINVAL, "offset^T lies in <w_B>: the coset meets the trace domain");
+        q.zinv_m[j] = to_mont(inv_std(z));
+    }
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    size_t sp = span_begin(ctx, "composition", (uint64_t)n * 8);
+    launch_fibsq_cp(ctx->trace_lde, ctx->scratch_c, q, s);
+    // coefficients: c_j = n^-1 offset^-j sum_i cp_i w^-ij   (fri_interpolate)
+    NttPlan ip{};
+    ip.log_n = L;
+    ip.tw = ctx->tw_inv;
+    launch_pow_table(ctx->pow_lo, ctx->pow_hi, L, inv_std(offset), inv_std((uint32_t)(n % P)), s);
+    ip.post_lo = ctx->pow_lo;
+    ip.post_hi = ctx->pow_hi;
+    launch_ntt(ip, ctx->scratch_c, n, ctx->scratch_b, s);
+    span_end(ctx, sp);
+    FRI_HIP(ctx, hipGetLastError());
+    int rc = run_commit(ctx, nullptr, ctx->scratch_b, n, L, offset, chan_in, flags, nullptr, out);
+    if (rc) return rc;
+    if (ctx->h_state->deg[0] > (int32_t)T)
+        return fail(ctx, FRI_EDEGREE, "composition polynomial degree exceeds T: the trace violates the constraints");
+    return FRI_OK;
+}
+
+extern "C" int fri_trace_decommit(fri_ctx* ctx, uint64_t index, uint64_t stride, uint32_t count, uint32_t* values,
+                                  uint8_t* paths, size_t paths_cap) {
+    if (!ctx || !values || !paths) return fail(ctx, FRI_EINVAL, "null argument");
+    if (!ctx->trace_valid) return fail(ctx, FRI_ESTATE, "no resident trace commit");
+    if (count < 1 || count > 8) return fail(ctx, FRI_EINVAL, "count must be 1..8");
+    const uint32_t L = ctx->trace_log_t + ctx->trace_log_b;
+    if (index >> L) return fail(ctx, FRI_EINVAL, "index out of range");
+    const size_t words = (size_t)count * 8 * L;
+    if (paths_cap < words * 4) return fail(ctx, FRI_EINVAL, "paths buffer too small (32 bytes per level per value)");
+    if (!ctx->dq_buf) FRI_HIP(ctx, hipMalloc(&ctx->dq_buf, 65536));
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    launch_trace_gather(ctx->trace_lde, ctx->trace_tree, L, index, stride, count, ctx->dq_buf, ctx->stream);
+    FRI_HIP(ctx, hipGetLastError());
+    std::vector<uint32_t> h(count + words);
+    FRI_HIP(ctx, hipMemcpyAsync(h.data(), ctx->dq_buf, h.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    memcpy(values, h.data(), count * 4);
+    memcpy(paths, h.data() + count, words * 4);
     return FRI_OK;
 }
 

@@ -119,4 +119,21 @@ void launch_permute_digests(const uint32_t* src, uint32_t* dst, uint32_t G, cons
 // nodes, <= 512) is already in t.tree; mx/G: coefficient maxima.
 void launch_top(const LayerTask& t, uint32_t l, const int32_t* mx, uint32_t G, hipStream_t s);
 
+// fri_prover.hip — STARK-101 FibonacciSq composition on the LDE coset.
+constexpr uint32_t FIBSQ_MAX_B = 16;   // blowup <= 2^4
+struct FibsqParams {
+    uint32_t log_n;              // LDE size n = B * T
+    uint32_t B;                  // blowup (power of two, 2..16): g = w_n^B
+    uint32_t offset_m;           // Montgomery(offset)
+    uint32_t w_m, winv_m;        // Montgomery(w_n^{+-1})
+    uint32_t glast_m, gprev_m;   // Montgomery(g^{T-1}), Montgomery(g^{T-2})
+    uint32_t a_last;             // canonical a_{T-1}
+    uint32_t alpha_m[3];         // Montgomery(alpha_0..2)
+    uint32_t zinv_m[FIBSQ_MAX_B];// Montgomery((offset^T w_B^j - 1)^-1), j < B
+};
+void launch_fibsq_cp(const uint32_t* f_lde, uint32_t* out, const FibsqParams& q, hipStream_t s);
+// out[j] = lde[(index + j*stride) mod 2^L], then count paths of L big-endian digests
+void launch_trace_gather(const uint32_t* lde, const uint32_t* tree, uint32_t L, uint64_t index, uint64_t stride,
+                         uint32_t count, uint32_t* out, hipStream_t s);
+
 }  // namespace fri

@@ -103,6 +103,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_auth_path": (i32, [vp, u32, ctypes.c_uint64, pu32, ctypes.c_char_p, ctypes.POINTER(u32)]),
         "fri_trace_commit": (i32, [vp, pu32, u32, u32, u32, ctypes.c_char_p, pu32, ctypes.POINTER(sz), pu32]),
         "fri_decommit_query": (i32, [vp, ctypes.c_uint64, pu32, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]),
+        "fri_fibsq_composition_commit": (i32, [vp, u32, u32, u32, u32, pu32, ctypes.POINTER(ChannelState), u32,
+                                               ctypes.POINTER(CommitResult)]),
+        "fri_trace_decommit": (i32, [vp, ctypes.c_uint64, ctypes.c_uint64, u32, pu32, ctypes.c_char_p, sz]),
         "fri_set_profiling": (i32, [vp, i32]),
         "fri_get_profile": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
@@ -246,20 +249,52 @@ class Context:
         self._check(self.lib.fri_auth_path(self.h, k, index, ctypes.byref(val), buf, ctypes.byref(dep)))
         return val.value, [buf.raw[32 * i: 32 * i + 32] for i in range(dep.value)]
 
-    def trace_commit(self, trace, log_blowup: int, offset: int = GENERATOR):
+    def trace_commit(self, trace, log_blowup: int, offset: int = GENERATOR, readback: bool = True):
         """fri_trace_commit: (LDE Merkle root bytes, trimmed trace-polynomial
-        coefficients, LDE values) for 2^log_t trace values."""
+        coefficients, LDE values) for 2^log_t trace values (coefficients and
+        LDE are None with readback=False: they stay on the device)."""
         tr = _u32(trace)
         log_t = tr.size.bit_length() - 1
         if tr.size != 1 << log_t:
             raise FriError(FRI_EINVAL, "trace length must be a power of two")
+        root = ctypes.create_string_buffer(32)
+        if not readback:
+            self._check(self.lib.fri_trace_commit(self.h, _ptr(tr), log_t, log_blowup, offset, root, None, None,
+                                                  None))
+            return root.raw, None, None
         coeffs = np.empty(tr.size, dtype=np.uint32)
         lde = np.empty(tr.size << log_blowup, dtype=np.uint32)
-        root = ctypes.create_string_buffer(32)
         ln = ctypes.c_size_t()
         self._check(self.lib.fri_trace_commit(self.h, _ptr(tr), log_t, log_blowup, offset, root, _ptr(coeffs),
                                               ctypes.byref(ln), _ptr(lde)))
         return root.raw, coeffs[: ln.value], lde
+
+    def fibsq_composition_commit(self, log_t: int, log_blowup: int, a_last: int, alphas: Sequence[int],
+                                 offset: int = GENERATOR, channel_state: Optional[bytes] = None,
+                                 graph: bool = True) -> CommitResult:
+        """fri_fibsq_composition_commit: composition polynomial of the resident
+        trace LDE, then the FRI commit of it (channel continued from
+        ``channel_state``)."""
+        al = _u32(alphas)
+        if al.size != 3:
+            raise FriError(FRI_EINVAL, "three alphas")
+        ch = ChannelState()
+        if channel_state:
+            ctypes.memmove(ch.digest, channel_state, 32)
+            ch.has_state = 1
+        res = CommitResult()
+        self._check(self.lib.fri_fibsq_composition_commit(self.h, log_t, log_blowup, offset, a_last, _ptr(al),
+                                                          ctypes.byref(ch), 0 if graph else FLAG_NO_GRAPH,
+                                                          ctypes.byref(res)))
+        return res
+
+    def trace_decommit(self, index: int, stride: int, count: int, depth: int):
+        """fri_trace_decommit: [(LDE[index + j*stride], path bytes)] for j < count."""
+        vals = np.empty(count, dtype=np.uint32)
+        buf = ctypes.create_string_buffer(32 * depth * count)
+        self._check(self.lib.fri_trace_decommit(self.h, index, stride, count, _ptr(vals), buf, len(buf)))
+        pl = 32 * depth
+        return [(int(vals[j]), buf.raw[j * pl:(j + 1) * pl]) for j in range(count)]
 
     def decommit_query(self, index: int, n_layers: int, log_n: int):
         """fri_decommit_query: per committed layer k, (value[idx], value[sib],
@@ -504,6 +539,19 @@ def verify_fri(messages: Sequence[bytes], log_n: int, n_layers: int, num_queries
     ``n_layers`` = number of committed layers (the reference's
     expected_num_layers). Returns False on any mismatch or malformed transcript.
     """
+    return _verify_transcript(messages, log_n, n_layers, num_queries, max_index, offset, channel_state)
+
+
+class _Reject(Exception):
+    pass
+
+
+def _verify_transcript(messages, log_n, n_layers, num_queries, max_index, offset, channel_state,
+                       pre_commit=None, on_query=None) -> bool:
+    """verify_fri's replay with two hooks for a STARK around the FRI:
+    ``pre_commit(take, ch)`` consumes the messages before the first FRI root;
+    ``on_query(take, ch, idx)`` those between a query index and its layer
+    openings, and returns the value layer 0 must hold at idx (or None)."""
     msgs = list(messages)
     pos = 0
 
@@ -516,6 +564,8 @@ def verify_fri(messages: Sequence[bytes], log_n: int, n_layers: int, num_queries
 
     try:
         ch = Channel(state=channel_state)
+        if pre_commit is not None:
+            pre_commit(take, ch)
         roots, betas = [], []
         for k in range(n_layers):
             r = take()
@@ -538,6 +588,7 @@ def verify_fri(messages: Sequence[bytes], log_n: int, n_layers: int, num_queries
             idx = ch.receive_random_int(0, max_index, True)
             if take() != idx.to_bytes(8, "big"):
                 return False
+            want0 = on_query(take, ch, idx) if on_query is not None else None
             prev = None                                  # (value at i, value at i + m/2, i, m) of layer k-1
             for k in range(n_layers):
                 m = 1 << (log_n - k)
@@ -558,6 +609,8 @@ def verify_fri(messages: Sequence[bytes], log_n: int, n_layers: int, num_queries
                     return False
                 if not (_merkle_path_ok(v, i, path, depth, roots[k]) and _merkle_path_ok(sv, sib, spath, depth, roots[k])):
                     return False
+                if k == 0 and want0 is not None and v != want0:
+                    return False
                 if prev is not None:
                     pa, pb, pj, pm = prev                    # pa = L[pj], pb = L[pj + pm/2]
                     x = pow(offset, 1 << (k - 1), P) * pow(pow(GENERATOR, (P - 1) // pm, P), pj, P) % P
@@ -569,8 +622,114 @@ def verify_fri(messages: Sequence[bytes], log_n: int, n_layers: int, num_queries
                 if k == n_layers - 1 and (v != final or sv != final):
                     return False
         return pos == len(msgs)
-    except (ValueError, IndexError, UnicodeDecodeError):
+    except (ValueError, IndexError, UnicodeDecodeError, _Reject):
         return False
+
+
+# ---- prover slice: STARK-101 FibonacciSq (BASELINE configs[3]) -------------
+# src/prover, src/trace, src/composition are empty in the reference; the
+# constraint system is STARK-101's (crate `stark-101`, Cargo.toml:2) on the
+# full trace subgroup; see include/fri_amd.h (fri_fibsq_composition_commit).
+
+def fibsq_trace(a1: int, T: int) -> List[int]:
+    """a_0 = 1, a_1 = a1, a_{i+2} = a_{i+1}^2 + a_i^2 (mod p), T rows."""
+    a = [1, a1 % P]
+    while len(a) < T:
+        a.append((a[-1] * a[-1] + a[-2] * a[-2]) % P)
+    return a[:T]
+
+
+@dataclass
+class StarkProof:
+    trace_root: bytes
+    alphas: List[int]
+    a_last: int
+    fri: FRIProof
+    log_t: int
+    log_blowup: int
+    queries: List[int]
+
+
+def prove_fibsq(a1: int, log_t: int, log_blowup: int, num_queries: int, channel: Channel,
+                offset: int = GENERATOR, ctx: Optional[Context] = None) -> StarkProof:
+    """STARK-101 prover on the GPU: trace -> LDE + Merkle (fri_trace_commit),
+    send the trace root, draw alpha_0..2, composition polynomial + FRI commit
+    (fri_fibsq_composition_commit), then per query (index drawn with
+    receive_random_int(0, n - 2B - 1, true)) send f(x), f(gx), f(g^2 x) with
+    their paths and the FRI layer openings (decommit_fri_layers,
+    fri_commit.rs:137-163).  The transcript is ``channel.proof``."""
+    L = log_t + log_blowup
+    B, n = 1 << log_blowup, 1 << L
+    ctx = ctx or _default_ctx(L)
+    trace = fibsq_trace(a1, 1 << log_t)
+    root, _, _ = ctx.trace_commit(trace, log_blowup, offset, readback=False)
+    channel.send(root.hex().encode())
+    alphas = [channel.receive_random_field_element() for _ in range(3)]
+    res = ctx.fibsq_composition_commit(log_t, log_blowup, trace[-1], alphas, offset,
+                                       channel_state=bytes.fromhex(channel.state))
+    fri = _mirror_commit(res, ctx, L, channel)
+    queries = []
+    for _ in range(num_queries):
+        idx = channel.receive_random_int(0, n - 2 * B - 1, True)
+        queries.append(idx)
+        for v, path in ctx.trace_decommit(idx, B, 3, L):
+            channel.send(v.to_bytes(8, "big"))
+            channel.send(path)
+        decommit_fri_layers(idx, fri, channel)
+    return StarkProof(root, alphas, trace[-1], fri, log_t, log_blowup, queries)
+
+
+def fibsq_cp_at(f0: int, f1: int, f2: int, x: int, alphas: Sequence[int], a_last: int, log_t: int) -> int:
+    """CP(x) from f(x), f(gx), f(g^2 x) (the composition the prover commits)."""
+    T = 1 << log_t
+    g = pow(GENERATOR, (P - 1) >> log_t, P)
+    glast, gprev = pow(g, T - 1, P), pow(g, T - 2, P)
+    p0 = (f0 - 1) * pow(x - 1, P - 2, P)
+    p1 = (f0 - a_last) * pow(x - glast, P - 2, P)
+    p2 = (f2 - f1 * f1 - f0 * f0) * (x - gprev) * (x - glast) * pow(pow(x, T, P) - 1, P - 2, P)
+    return (alphas[0] * p0 + alphas[1] * p1 + alphas[2] * p2) % P
+
+
+def verify_fibsq(messages: Sequence[bytes], a_last: int, log_t: int, log_blowup: int, num_queries: int,
+                 n_layers: int, offset: int = GENERATOR, channel_state: str = "") -> bool:
+    """Verifier of prove_fibsq's transcript: replays the channel (trace root,
+    alphas, FRI roots/betas/final, query indices), checks every trace path
+    against the trace root, that layer 0 at each query equals the composition
+    polynomial computed from the opened f(x), f(gx), f(g^2 x), and then every
+    FRI check of verify_fri."""
+    L = log_t + log_blowup
+    B, n = 1 << log_blowup, 1 << L
+    state = {}
+
+    def pre_commit(take, ch):
+        r = take()
+        if len(r) != 64:
+            raise _Reject()
+        state["root"] = bytes.fromhex(r.decode())
+        ch.send(r)
+        al = []
+        for _ in range(3):
+            a = ch.receive_random_field_element()
+            if take() != a.to_bytes(8, "big"):
+                raise _Reject()
+            al.append(a)
+        state["alphas"] = al
+
+    def on_query(take, ch, idx):
+        fs = []
+        for j in range(3):
+            vb, path = take(), take()
+            ch.send(vb)
+            ch.send(path)
+            v = int.from_bytes(vb, "big")
+            if len(vb) != 8 or v >= P or not _merkle_path_ok(v, idx + j * B, path, L, state["root"]):
+                raise _Reject()
+            fs.append(v)
+        x = offset * pow(pow(GENERATOR, (P - 1) >> L, P), idx, P) % P
+        return fibsq_cp_at(fs[0], fs[1], fs[2], x, state["alphas"], a_last, log_t)
+
+    return _verify_transcript(messages, L, n_layers, num_queries, n - 2 * B - 1, offset, channel_state,
+                              pre_commit, on_query)
 
 
 _CTX_CACHE = {}
@@ -596,6 +755,12 @@ def fri_commit(coeffs: Sequence[int], log_n: int, channel: Channel, offset: int 
     ctx = ctx or _default_ctx(log_n)
     st = bytes.fromhex(channel.state) if channel.state else None
     res = ctx.commit(coeffs, log_n, offset, channel_state=st)
+    return _mirror_commit(res, ctx, log_n, channel)
+
+
+def _mirror_commit(res: CommitResult, ctx: Context, log_n: int, channel: Channel) -> FRIProof:
+    """Append the messages the device commit sent (root hex per layer, beta
+    per round, final value) to ``channel`` and take over its state."""
     roots = [bytes(res.roots[k]) for k in range(res.n_layers)]
     betas = [int(res.betas[r]) for r in range(res.n_rounds)]
     for k, root in enumerate(roots):

@@ -7,7 +7,7 @@ The reference (Rust, nightly, crates not vendored) cannot be built or run in
 this image, so these vectors are this repo's frozen-spec
 restatement, cross-checked against the independent C oracle by
 tests/test_oracle_crosscheck.py.  Layers are stored as SHA-256 of their little-endian
-u32 bytes plus the first 8 values.  "decommit_q3" continues each case's
+u32 bytes plus the first 8 values.  "fibsq" holds prover-slice transcripts (fo.fibsq_prove).  "decommit_q3" continues each case's
 channel with decommit_fri(3, n - 1, ...) (fri_commit.rs:137-179): the state
 after it, and the SHA-256 of the proof messages it appended.
 """
@@ -53,7 +53,30 @@ def case(name, coeffs, log_n, state="", forced=None, offset=fo.GEN):
     }
 
 
+def proof_sha(msgs):
+    return hashlib.sha256(b"".join(len(m).to_bytes(4, "little") + m for m in msgs)).hexdigest()
+
+
+def fibsq_case(name, a1, log_t, log_b, queries, state=""):
+    """Prover slice (STARK-101 FibonacciSq, fo.fibsq_prove): the whole
+    transcript of trace commit, alphas, FRI commit of the composition
+    polynomial and `queries` decommitments."""
+    ch = fo.Channel(state=state)
+    pr = fo.fibsq_prove(a1, log_t, log_b, queries, ch)
+    return {
+        "name": name, "a1": a1, "log_t": log_t, "log_blowup": log_b, "queries": queries, "channel_in": state,
+        "trace_root": pr.trace_root.hex(), "alphas": pr.alphas, "a_last": fo.fibsq_trace(a1, 1 << log_t)[-1],
+        "roots": [x.hex() for x in pr.fri.roots], "betas": pr.fri.betas, "final_value": pr.fri.final_value,
+        "final_degree": pr.fri.final_degree, "n_layers": len(pr.fri.roots), "query_indices": pr.queries,
+        "channel_out": ch.state, "messages": len(ch.proof), "proof_sha256": proof_sha(ch.proof),
+    }
+
+
 def main():
+    fibsq = [fibsq_case("stark101_t8_b8", 3141592, 3, 3, 3), fibsq_case("stark101_t32_b8", 3141592, 5, 3, 3),
+             fibsq_case("stark101_t64_b8", 3141592, 6, 3, 4), fibsq_case("a1_7_t16_b2", 7, 4, 1, 2),
+             fibsq_case("a1_big_t32_b4", fo.P - 2, 5, 2, 3),
+             fibsq_case("prefilled_t16_b16", 12345, 4, 4, 2, state=hashlib.sha256(b"public-input").hexdigest())]
     cases = []
     for log_n in range(3, 12):
         for seed in (42, 43, 44):
@@ -80,7 +103,7 @@ def main():
     cases.append(case("forced_betas", fo.splitmix64_field(12, 16), 7, forced=list(range(1, 33))))
     out = os.path.join(HERE, "fri_golden.json")
     with open(out, "w") as f:
-        json.dump({"p": fo.P, "generator": fo.GEN, "cases": cases}, f, indent=1)
+        json.dump({"p": fo.P, "generator": fo.GEN, "cases": cases, "fibsq": fibsq}, f, indent=1)
     print(f"wrote {len(cases)} cases to {out}")
 
 
