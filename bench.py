@@ -293,6 +293,14 @@ def main():
                        "what": "fri_trace_commit: 2^16 trace -> iNTT -> LDE on 5*<w_2^19> -> SHA-256 Merkle "
                                "(host trace in, root + coefficients + LDE read back)"}
 
+    # Whole prover slice, BASELINE configs[3]: STARK-101 FibonacciSq trace of
+    # 2^16 rows -> LDE 2^19 + Merkle -> alphas -> composition polynomial ->
+    # FRI commit -> 3 queries (trace + FRI decommitments); host trace in,
+    # transcript out.  Reported beside the metric, never `value`.
+    prover = None
+    if world == 1 and log_n >= 19:
+        prover = _prover_stage(ctx, fri_amd, with_cpu=(rank == 0 and not args.no_cpu_baseline))
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = _cpu_baseline(coeffs, d, log_n)
@@ -320,6 +328,7 @@ def main():
             "breakdown_ms_per_step": breakdown,
             "pcie_inclusive": pcie,
             "prover_trace_commit": trace_stage,
+            "prover_fibsq": prover,
             "cpu_baseline": cpu,
         }
         if note:
@@ -330,6 +339,44 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _prover_stage(ctx, fri_amd, with_cpu, log_t=16, log_b=3, queries=3, a1=3141592):
+    ch = fri_amd.Channel()
+    pr = fri_amd.prove_fibsq(a1, log_t, log_b, queries, ch, ctx=ctx)        # warm-up + plan build
+    ok = fri_amd.verify_fibsq(ch.proof, pr.a_last, log_t, log_b, queries, len(pr.fri.roots))
+    k = 5
+    t0 = time.perf_counter()
+    for _ in range(k):
+        fri_amd.prove_fibsq(a1, log_t, log_b, queries, fri_amd.Channel(), ctx=ctx)
+    ms = 1000.0 * (time.perf_counter() - t0) / k
+    out = {"ms_per_proof": round(ms, 4), "verified": bool(ok), "fri_layers": len(pr.fri.roots),
+           "proof_messages": len(ch.proof), "proof_bytes": ch.proof_size(),
+           "what": f"STARK-101 FibonacciSq prover: trace 2^{log_t} -> LDE 2^{log_t + log_b} + Merkle -> alphas -> "
+                   f"composition polynomial -> FRI commit ({len(pr.fri.roots)} layers) -> {queries} queries; "
+                   f"host trace in, transcript out (BASELINE configs[3])"}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        try:
+            import fri_oracle as fo
+            lib = fo.load_c_oracle()
+            och = fo.OrcChannel()
+            lib.orc_channel_init(ctypes.byref(och))
+            root = ctypes.create_string_buffer(32)
+            al = (ctypes.c_uint64 * 3)()
+            r = fo.OrcFriResult()
+            t0 = time.perf_counter()
+            lib.orc_fibsq_prove_commit(a1, log_t, log_b, 5, 5, fo.P, ctypes.byref(och), root, al, ctypes.byref(r),
+                                       None, None, None, None)
+            t = time.perf_counter() - t0
+            out["cpu_baseline"] = {"ms_per_proof": round(1000.0 * t, 2), "cores": lib.orc_num_threads(),
+                                   "kind": "port", "matches_gpu": root.raw == pr.trace_root and
+                                   [bytes(r.roots[j]) for j in range(r.n_layers)] == pr.fri.roots,
+                                   "sample": "OpenMP C restatement of the commit phase (trace LDE + Merkle, "
+                                             "composition, FRI), queries excluded"}
+        except Exception as e:  # noqa: BLE001
+            out["cpu_baseline"] = {"error": str(e)}
+    return out
 
 
 def _pmc_traffic(log_n):

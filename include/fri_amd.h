@@ -156,6 +156,11 @@ int fri_fibsq_composition_commit(fri_ctx* ctx, uint32_t log_t, uint32_t log_blow
                                  const fri_channel_state* chan_in, uint32_t flags,
                                  fri_commit_result* out);
 
+/* The FibonacciSq trace itself: out[0] = 1, out[1] = a1,
+ * out[i+2] = out[i+1]^2 + out[i]^2 mod p, 2^log_t rows.  Host-side (a serial
+ * recurrence); needs no context or device.  a1 must be canonical. */
+int fri_fibsq_trace(uint32_t a1, uint32_t log_t, uint32_t* out);
+
 /* Trace-tree decommitment (STARK-101 decommit_on_query: f(x), f(gx), f(g^2x)
  * with their paths): values[j] = LDE[(index + j*stride) mod n], j < count
  * (1..8); paths = count authentication paths of log2(n) sibling digests

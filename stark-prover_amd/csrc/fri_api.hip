@@ -101,6 +101,7 @@ struct fri_ctx {
     hipEvent_t ev_pre = nullptr, ev_coef = nullptr;
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
     uint32_t* dq_buf = nullptr;     // decommitment gather staging (64 KiB)
+    uint32_t* dq_host = nullptr;    // ... and its pinned host mirror (one DMA per query)
     uint32_t* trace_tree = nullptr; // Merkle tree of the last fri_trace_commit LDE
     uint32_t* trace_lde = nullptr;  // ... and the LDE itself (prover: composition, queries)
     size_t trace_tree_cap = 0;      // leaves they can hold
@@ -230,6 +231,7 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     hipFree(ctx->pow_lo); hipFree(ctx->pow_hi);
     hipFree(ctx->d_state);
     hipFree(ctx->dq_buf);
+    if (ctx->dq_host) hipHostFree(ctx->dq_host);
     hipFree(ctx->trace_tree);
     hipFree(ctx->trace_lde);
     if (ctx->h_state) hipHostFree(ctx->h_state);
@@ -745,6 +747,13 @@ extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint3
     return FRI_OK;
 }
 
+// 64 KiB device staging + pinned host mirror for the per-query gathers.
+static int dq_alloc(fri_ctx* ctx) {
+    if (!ctx->dq_buf) FRI_HIP(ctx, hipMalloc(&ctx->dq_buf, 65536));
+    if (!ctx->dq_host) FRI_HIP(ctx, hipHostMalloc(&ctx->dq_host, 65536, hipHostMallocDefault));
+    return FRI_OK;
+}
+
 extern "C" int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap,
                                   uint8_t* paths, size_t paths_cap, size_t* paths_len) {
     if (!ctx || !values || !paths_len) return fail(ctx, FRI_EINVAL, "null argument");
@@ -767,16 +776,16 @@ extern "C" int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values
     if (values_cap < 2 * (size_t)dp.n_layers) return fail(ctx, FRI_EINVAL, "values buffer too small (2 per layer)");
     if (!paths || paths_cap < (size_t)words * 4) return fail(ctx, FRI_EINVAL, "paths buffer too small (see paths_len)");
     const size_t total = (2 * (size_t)dp.n_layers + words) * 4;
-    if (!ctx->dq_buf) FRI_HIP(ctx, hipMalloc(&ctx->dq_buf, 65536));
     if (total > 65536) return fail(ctx, FRI_EINVAL, "decommitment too large");
     FRI_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = dq_alloc(ctx);
+    if (rc) return rc;
     launch_decommit_gather(p.layers, p.trees, dp, ctx->dq_buf, ctx->stream);
     FRI_HIP(ctx, hipGetLastError());
-    std::vector<uint32_t> h(total / 4);
-    FRI_HIP(ctx, hipMemcpyAsync(h.data(), ctx->dq_buf, total, hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->dq_host, ctx->dq_buf, total, hipMemcpyDeviceToHost, ctx->stream));
     FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    memcpy(values, h.data(), 2 * dp.n_layers * 4);
-    memcpy(paths, h.data() + 2 * dp.n_layers, (size_t)words * 4);
+    memcpy(values, ctx->dq_host, 2 * dp.n_layers * 4);
+    memcpy(paths, ctx->dq_host + 2 * dp.n_layers, (size_t)words * 4);
     return FRI_OK;
 }
 
@@ -840,6 +849,25 @@ extern "C" int fri_fibsq_composition_commit(fri_ctx* ctx, uint32_t log_t, uint32
     return FRI_OK;
 }
 
+// STARK-101 FibonacciSq trace.  The recurrence is one serial dependency
+// chain (each row needs the previous two), so it runs on the host: ~2
+// 64-bit mulmods per row, far below one kernel launch for any T here.
+extern "C" int fri_fibsq_trace(uint32_t a1, uint32_t log_t, uint32_t* out) {
+    if (!out || log_t > 30) return FRI_EINVAL;
+    if (a1 >= P) return FRI_EINVAL;
+    const size_t T = (size_t)1 << log_t;
+    uint64_t x = 1, y = a1;
+    out[0] = 1;
+    if (T > 1) out[1] = a1;
+    for (size_t i = 2; i < T; i++) {
+        const uint64_t z = (x * x % P + y * y % P) % P;
+        out[i] = (uint32_t)z;
+        x = y;
+        y = z;
+    }
+    return FRI_OK;
+}
+
 extern "C" int fri_trace_decommit(fri_ctx* ctx, uint64_t index, uint64_t stride, uint32_t count, uint32_t* values,
                                   uint8_t* paths, size_t paths_cap) {
     if (!ctx || !values || !paths) return fail(ctx, FRI_EINVAL, "null argument");
@@ -849,15 +877,15 @@ extern "C" int fri_trace_decommit(fri_ctx* ctx, uint64_t index, uint64_t stride,
     if (index >> L) return fail(ctx, FRI_EINVAL, "index out of range");
     const size_t words = (size_t)count * 8 * L;
     if (paths_cap < words * 4) return fail(ctx, FRI_EINVAL, "paths buffer too small (32 bytes per level per value)");
-    if (!ctx->dq_buf) FRI_HIP(ctx, hipMalloc(&ctx->dq_buf, 65536));
     FRI_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = dq_alloc(ctx);
+    if (rc) return rc;
     launch_trace_gather(ctx->trace_lde, ctx->trace_tree, L, index, stride, count, ctx->dq_buf, ctx->stream);
     FRI_HIP(ctx, hipGetLastError());
-    std::vector<uint32_t> h(count + words);
-    FRI_HIP(ctx, hipMemcpyAsync(h.data(), ctx->dq_buf, h.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->dq_host, ctx->dq_buf, (count + words) * 4, hipMemcpyDeviceToHost, ctx->stream));
     FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    memcpy(values, h.data(), count * 4);
-    memcpy(paths, h.data() + count, words * 4);
+    memcpy(values, ctx->dq_host, count * 4);
+    memcpy(paths, ctx->dq_host + count, words * 4);
     return FRI_OK;
 }
 

@@ -105,6 +105,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_decommit_query": (i32, [vp, ctypes.c_uint64, pu32, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]),
         "fri_fibsq_composition_commit": (i32, [vp, u32, u32, u32, u32, pu32, ctypes.POINTER(ChannelState), u32,
                                                ctypes.POINTER(CommitResult)]),
+        "fri_fibsq_trace": (i32, [u32, u32, pu32]),
         "fri_trace_decommit": (i32, [vp, ctypes.c_uint64, ctypes.c_uint64, u32, pu32, ctypes.c_char_p, sz]),
         "fri_set_profiling": (i32, [vp, i32]),
         "fri_get_profile": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -631,12 +632,17 @@ def _verify_transcript(messages, log_n, n_layers, num_queries, max_index, offset
 # constraint system is STARK-101's (crate `stark-101`, Cargo.toml:2) on the
 # full trace subgroup; see include/fri_amd.h (fri_fibsq_composition_commit).
 
-def fibsq_trace(a1: int, T: int) -> List[int]:
-    """a_0 = 1, a_1 = a1, a_{i+2} = a_{i+1}^2 + a_i^2 (mod p), T rows."""
-    a = [1, a1 % P]
-    while len(a) < T:
-        a.append((a[-1] * a[-1] + a[-2] * a[-2]) % P)
-    return a[:T]
+def fibsq_trace(a1: int, T: int) -> np.ndarray:
+    """a_0 = 1, a_1 = a1, a_{i+2} = a_{i+1}^2 + a_i^2 (mod p), T = 2^k rows
+    (fri_fibsq_trace, host-side: the recurrence is one serial chain)."""
+    log_t = T.bit_length() - 1
+    if T != 1 << log_t:
+        raise FriError(FRI_EINVAL, "trace length must be a power of two")
+    out = np.empty(T, dtype=np.uint32)
+    rc = load_library().fri_fibsq_trace(a1 % P, log_t, _ptr(out))
+    if rc != FRI_OK:
+        raise FriError(rc, "fri_fibsq_trace")
+    return out
 
 
 @dataclass
@@ -665,7 +671,7 @@ def prove_fibsq(a1: int, log_t: int, log_blowup: int, num_queries: int, channel:
     root, _, _ = ctx.trace_commit(trace, log_blowup, offset, readback=False)
     channel.send(root.hex().encode())
     alphas = [channel.receive_random_field_element() for _ in range(3)]
-    res = ctx.fibsq_composition_commit(log_t, log_blowup, trace[-1], alphas, offset,
+    res = ctx.fibsq_composition_commit(log_t, log_blowup, int(trace[-1]), alphas, offset,
                                        channel_state=bytes.fromhex(channel.state))
     fri = _mirror_commit(res, ctx, L, channel)
     queries = []
@@ -676,12 +682,13 @@ def prove_fibsq(a1: int, log_t: int, log_blowup: int, num_queries: int, channel:
             channel.send(v.to_bytes(8, "big"))
             channel.send(path)
         decommit_fri_layers(idx, fri, channel)
-    return StarkProof(root, alphas, trace[-1], fri, log_t, log_blowup, queries)
+    return StarkProof(root, alphas, int(trace[-1]), fri, log_t, log_blowup, queries)
 
 
 def fibsq_cp_at(f0: int, f1: int, f2: int, x: int, alphas: Sequence[int], a_last: int, log_t: int) -> int:
     """CP(x) from f(x), f(gx), f(g^2 x) (the composition the prover commits)."""
     T = 1 << log_t
+    f0, f1, f2, x, a_last = int(f0), int(f1), int(f2), int(x), int(a_last)
     g = pow(GENERATOR, (P - 1) >> log_t, P)
     glast, gprev = pow(g, T - 1, P), pow(g, T - 2, P)
     p0 = (f0 - 1) * pow(x - 1, P - 2, P)
@@ -699,6 +706,7 @@ def verify_fibsq(messages: Sequence[bytes], a_last: int, log_t: int, log_blowup:
     FRI check of verify_fri."""
     L = log_t + log_blowup
     B, n = 1 << log_blowup, 1 << L
+    a_last = int(a_last)
     state = {}
 
     def pre_commit(take, ch):

@@ -119,9 +119,9 @@ def test_composition_detects_constraint_violation(ctx):
     trace = fri_amd.fibsq_trace(3141592, 1 << log_t)
     ctx.trace_commit(trace, lb, readback=False)
     with pytest.raises(fri_amd.FriError) as e:
-        ctx.fibsq_composition_commit(log_t, lb, (trace[-1] + 1) % P, [1, 2, 3], channel_state=bytes(32))
+        ctx.fibsq_composition_commit(log_t, lb, (int(trace[-1]) + 1) % P, [1, 2, 3], channel_state=bytes(32))
     assert e.value.code == fri_amd.FRI_EDEGREE
-    res = ctx.fibsq_composition_commit(log_t, lb, trace[-1], [1, 2, 3], channel_state=bytes(32))
+    res = ctx.fibsq_composition_commit(log_t, lb, int(trace[-1]), [1, 2, 3], channel_state=bytes(32))
     assert res.n_rounds == log_t + 1
 
 
@@ -130,7 +130,7 @@ def test_prover_entry_errors(ctx):
     trace = fri_amd.fibsq_trace(7, 1 << 8)
     ctx.trace_commit(trace, 3, readback=False)
     with pytest.raises(fri_amd.FriError) as e:          # other (log_t, blowup) than the resident trace
-        ctx.fibsq_composition_commit(9, 3, trace[-1], [1, 2, 3])
+        ctx.fibsq_composition_commit(9, 3, int(trace[-1]), [1, 2, 3])
     assert e.value.code == fri_amd.FRI_ESTATE
     with pytest.raises(fri_amd.FriError) as e:
         ctx.trace_decommit(1 << 11, 8, 3, 11)             # index beyond the LDE

@@ -34,6 +34,13 @@ def test_fibsq_trace_recurrence(oracle, corc):
     assert list(out) == t
 
 
+def test_library_trace_generator_matches_oracle(oracle):
+    """fri_fibsq_trace is host code in libfri_amd.so (no device needed)."""
+    import fri_amd
+    for a1, log_t in ((3141592, 10), (P - 1, 4), (0, 3), (7, 1)):
+        assert fri_amd.fibsq_trace(a1, 1 << log_t).tolist() == oracle.fibsq_trace(a1, 1 << log_t)
+
+
 def test_python_twin_reproduces_golden_prover_transcripts(oracle, golden):
     for c in golden["fibsq"]:
         ch = oracle.Channel(state=c["channel_in"])
