@@ -151,6 +151,7 @@ class Context:
         if rc != FRI_OK:
             raise FriError(rc, "fri_ctx_create failed (no gfx950 device?)")
         self.h = h
+        self.device = device
         self.log_n_max = log_n_max
 
     def close(self):
