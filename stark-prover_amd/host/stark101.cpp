@@ -5,6 +5,8 @@
 // turns fri_commit_result into Channel messages and an FRIProof.
 #include "stark101.hpp"
 
+#include <functional>
+
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -236,6 +238,11 @@ FRIProof fri_commit_coset(const Poly& poly, uint32_t log_n, FE offset, FriChanne
                           0, nullptr, &res),
                "fri_commit");
 
+    return FRIProof::mirror(res, log_n, gpu, channel);
+}
+
+FRIProof FRIProof::mirror(const fri_commit_result& res, uint32_t log_n, const std::shared_ptr<Gpu>& gpu,
+                          FriChannel& channel) {
     // The channel messages the reference's loop produced (fri_commit.rs:84-114):
     // root_hex bytes per layer, beta (8 B BE, proof only) per round, final value.
     FRIProof proof;
@@ -346,17 +353,27 @@ uint64_t be_u64(const std::vector<uint8_t>& b) {
 }
 }  // namespace
 
-bool verify_fri(const std::vector<std::vector<uint8_t>>& msgs, uint32_t log_n, size_t n_layers, size_t num_queries,
-                size_t max_index, FE offset, const std::string& channel_state) {
+namespace {
+using Msgs = std::vector<std::vector<uint8_t>>;
+using Take = std::function<const std::vector<uint8_t>&()>;
+// verify_fri's replay with two hooks for a STARK around the FRI:
+// pre_commit consumes the messages before the first FRI root; on_query those
+// between a query index and its layer openings and returns the value layer 0
+// must hold there (or -1).  A hook rejects by throwing Panic.
+bool verify_transcript(const Msgs& msgs, uint32_t log_n, size_t n_layers, size_t num_queries, size_t max_index,
+                       FE offset, const std::string& channel_state,
+                       const std::function<void(const Take&, FriChannel&)>& pre_commit,
+                       const std::function<int64_t(const Take&, FriChannel&, uint64_t)>& on_query) {
     if (n_layers == 0 || n_layers > log_n + 1u) return false;
     size_t pos = 0;
-    auto take = [&]() -> const std::vector<uint8_t>& {
+    Take take = [&]() -> const std::vector<uint8_t>& {
         if (pos >= msgs.size()) throw Panic("transcript ended early");
         return msgs[pos++];
     };
     try {
         FriChannel ch;
         ch.state = channel_state;
+        if (pre_commit) pre_commit(take, ch);
         std::vector<std::array<uint8_t, 32>> roots;
         std::vector<FE> betas;
         for (size_t k = 0; k < n_layers; k++) {
@@ -381,6 +398,7 @@ bool verify_fri(const std::vector<std::vector<uint8_t>>& msgs, uint32_t log_n, s
         for (size_t q = 0; q < num_queries; q++) {
             const uint64_t idx = ch.receive_random_int(0, max_index, true);
             if (take() != FriChannel::be64(idx)) return false;
+            const int64_t want0 = on_query ? on_query(take, ch, idx) : -1;
             bool have_prev = false;
             uint64_t pa = 0, pb = 0, pj = 0, pm = 0;           // L[pj], L[pj + pm/2] of layer k-1
             for (size_t k = 0; k < n_layers; k++) {
@@ -402,6 +420,7 @@ bool verify_fri(const std::vector<std::vector<uint8_t>>& msgs, uint32_t log_n, s
                 const uint64_t v = be_u64(vb), sv = be_u64(sb);
                 if (v >= P || sv >= P) return false;
                 if (!path_ok(v, i, path, depth, roots[k]) || !path_ok(sv, sib, spath, depth, roots[k])) return false;
+                if (k == 0 && want0 >= 0 && v != static_cast<uint64_t>(want0)) return false;
                 if (have_prev) {
                     // x = offset^(2^(k-1)) * omega_pm^pj; fold = (a+b)/2 + beta*(a-b)/(2x)  (fri_commit.rs:32-65)
                     const FE x = offset.pow(uint64_t{1} << (k - 1)) * omega(ceil_log2(pm)).pow(pj);
@@ -422,6 +441,110 @@ bool verify_fri(const std::vector<std::vector<uint8_t>>& msgs, uint32_t log_n, s
         return false;
     }
 }
+}  // namespace
+
+bool verify_fri(const Msgs& msgs, uint32_t log_n, size_t n_layers, size_t num_queries, size_t max_index, FE offset,
+                const std::string& channel_state) {
+    return verify_transcript(msgs, log_n, n_layers, num_queries, max_index, offset, channel_state, nullptr, nullptr);
+}
+
+// ----------------------------------------------------------- prover slice
+std::vector<FE> fibsq_trace(FE a1, uint32_t log_t) {
+    std::vector<uint32_t> t(size_t{1} << log_t);
+    if (fri_fibsq_trace(static_cast<uint32_t>(a1.value()), log_t, t.data()) != FRI_OK) throw Panic("fri_fibsq_trace");
+    return to_fe(t.data(), t.size());
+}
+
+StarkProof prove_fibsq(FE a1, uint32_t log_t, uint32_t log_blowup, size_t num_queries, FriChannel& channel, FE offset,
+                       std::shared_ptr<Gpu> gpu) {
+    const uint32_t L = log_t + log_blowup;
+    const uint64_t B = uint64_t{1} << log_blowup, n = uint64_t{1} << L;
+    if (!gpu) gpu = Gpu::thread_default(L);
+    if (L > gpu->log_n_max()) throw Panic("prove_fibsq: LDE 2^" + std::to_string(L) + " exceeds the context");
+    std::vector<uint32_t> trace(size_t{1} << log_t);
+    gpu->check(fri_fibsq_trace(static_cast<uint32_t>(a1.value()), log_t, trace.data()), "fri_fibsq_trace");
+    StarkProof sp;
+    sp.log_t = log_t;
+    sp.log_blowup = log_blowup;
+    sp.a_last = FE(trace.back());
+    const uint32_t off = static_cast<uint32_t>(offset.value());
+    gpu->check(fri_trace_commit(gpu->ctx(), trace.data(), log_t, log_blowup, off, sp.trace_root.data(), nullptr,
+                                nullptr, nullptr),
+               "fri_trace_commit");
+    const std::string root_hex = sha::hex(sp.trace_root.data(), 32);
+    channel.send(reinterpret_cast<const uint8_t*>(root_hex.data()), root_hex.size());
+    for (auto& a : sp.alphas) a = channel.receive_random_field_element();
+    fri_channel_state cin{};
+    auto st = sha::from_hex(channel.state);
+    std::memcpy(cin.digest, st.data(), 32);
+    cin.has_state = 1;
+    const uint32_t al[3] = {static_cast<uint32_t>(sp.alphas[0].value()), static_cast<uint32_t>(sp.alphas[1].value()),
+                            static_cast<uint32_t>(sp.alphas[2].value())};
+    fri_commit_result res{};
+    gpu->bump();
+    gpu->check(fri_fibsq_composition_commit(gpu->ctx(), log_t, log_blowup, off, trace.back(), al, &cin, 0, &res),
+               "fri_fibsq_composition_commit");
+    sp.fri = FRIProof::mirror(res, L, gpu, channel);
+    std::vector<uint32_t> vals(3);
+    std::vector<uint8_t> paths(3 * 32 * size_t{L});
+    for (size_t q = 0; q < num_queries; q++) {
+        const uint64_t idx = channel.receive_random_int(0, n - 2 * B - 1, true);
+        sp.queries.push_back(idx);
+        gpu->check(fri_trace_decommit(gpu->ctx(), idx, B, 3, vals.data(), paths.data(), paths.size()),
+                   "fri_trace_decommit");
+        for (size_t j = 0; j < 3; j++) {
+            channel.send(FE(vals[j]).to_bytes());
+            channel.send(paths.data() + 32 * L * j, 32 * size_t{L});
+        }
+        decommit_fri_layers(idx, sp.fri, channel);
+    }
+    return sp;
+}
+
+FE fibsq_composition_at(FE f0, FE f1, FE f2, FE x, const std::array<FE, 3>& alphas, FE a_last, uint32_t log_t) {
+    const uint64_t T = uint64_t{1} << log_t;
+    const FE g = omega(log_t), glast = g.pow(T - 1), gprev = g.pow(T - 2);
+    const FE p0 = (f0 - FE(1)) * (x - FE(1)).inverse();
+    const FE p1 = (f0 - a_last) * (x - glast).inverse();
+    const FE p2 = (f2 - f1 * f1 - f0 * f0) * (x - gprev) * (x - glast) * (x.pow(T) - FE(1)).inverse();
+    return alphas[0] * p0 + alphas[1] * p1 + alphas[2] * p2;
+}
+
+bool verify_fibsq(const Msgs& msgs, FE a_last, uint32_t log_t, uint32_t log_blowup, size_t num_queries,
+                  size_t n_layers, FE offset, const std::string& channel_state) {
+    const uint32_t L = log_t + log_blowup;
+    const uint64_t B = uint64_t{1} << log_blowup, n = uint64_t{1} << L;
+    std::array<uint8_t, 32> root{};
+    std::array<FE, 3> alphas{};
+    auto pre = [&](const Take& take, FriChannel& ch) {
+        const auto& r = take();
+        if (r.size() != 64) throw Panic("trace root");
+        auto rb = sha::from_hex(std::string(r.begin(), r.end()));
+        std::memcpy(root.data(), rb.data(), 32);
+        ch.send(r);
+        for (auto& a : alphas) {
+            a = ch.receive_random_field_element();
+            if (take() != FriChannel::be64(a.value())) throw Panic("alpha");
+        }
+    };
+    auto on_query = [&](const Take& take, FriChannel& ch, uint64_t idx) -> int64_t {
+        FE f[3];
+        for (int j = 0; j < 3; j++) {
+            const auto& vb = take();
+            const auto& path = take();
+            ch.send(vb);
+            ch.send(path);
+            if (vb.size() != 8) throw Panic("trace value");
+            const uint64_t v = be_u64(vb);
+            if (v >= P || !path_ok(v, idx + j * B, path, L, root)) throw Panic("trace path");
+            f[j] = FE(v);
+        }
+        const FE x = offset * omega(L).pow(idx);
+        return static_cast<int64_t>(fibsq_composition_at(f[0], f[1], f[2], x, alphas, a_last, log_t).value());
+    };
+    return verify_transcript(msgs, L, n_layers, num_queries, n - 2 * B - 1, offset, channel_state, pre, on_query);
+}
+
 
 // ------------------------------------------------------- polynomial layer
 std::vector<FE> evaluate_on_coset(const Poly& poly, const Coset& coset) {

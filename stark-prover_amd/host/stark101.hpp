@@ -270,6 +270,7 @@ class Gpu {
 };
 
 class FRIProof;
+struct StarkProof;
 
 // merkle/mod.rs:5-27.  A standalone tree keeps only its root; the trees of
 // an FRIProof stay in HBM and also serve authentication paths.
@@ -308,6 +309,12 @@ class FRIProof {
   private:
     friend FRIProof fri_commit_coset(const Poly&, uint32_t, FE, FriChannel&, const std::shared_ptr<Gpu>&);
     friend void decommit_fri_layers(size_t, const FRIProof&, FriChannel&);
+    friend StarkProof prove_fibsq(FE, uint32_t, uint32_t, size_t, FriChannel&, FE, std::shared_ptr<Gpu>);
+    // The proof of a device commit: appends the messages the device sent
+    // (root hex per layer, beta per round, final value) to `channel` and
+    // takes over its state (fri_commit.rs:84-114).
+    static FRIProof mirror(const fri_commit_result& res, uint32_t log_n, const std::shared_ptr<Gpu>& gpu,
+                           FriChannel& channel);
     std::shared_ptr<Gpu> gpu_;
     uint64_t gen_ = 0;
     void require_resident() const;
@@ -339,6 +346,35 @@ void decommit_fri(size_t num_queries, size_t max_index, const FRIProof& proof, F
 bool verify_fri(const std::vector<std::vector<uint8_t>>& messages, uint32_t log_n, size_t n_layers,
                 size_t num_queries, size_t max_index, FE offset = FE(FRI_GENERATOR),
                 const std::string& channel_state = "");
+
+// ------------------------------------------------ prover slice (configs[3])
+// src/prover, src/trace and src/composition are empty in the reference; the
+// constraint system is STARK-101's FibonacciSq on the full trace subgroup
+// (include/fri_amd.h, fri_fibsq_composition_commit):
+//   a_0 = 1, a_1 = a1, a_{i+2} = a_{i+1}^2 + a_i^2;  public output a_{T-1}.
+// prove_fibsq: trace -> LDE + Merkle (GPU) -> send(root hex) -> alpha_0..2
+// -> composition polynomial + its FRI commit (GPU) -> per query
+// idx = receive_random_int(0, n - 2B - 1, true): f(x), path, f(gx), path,
+// f(g^2x), path, then decommit_fri_layers (fri_commit.rs:137-163).
+struct StarkProof {
+    std::array<uint8_t, 32> trace_root{};
+    std::array<FE, 3> alphas{};
+    FE a_last;
+    FRIProof fri;
+    uint32_t log_t = 0, log_blowup = 0;
+    std::vector<uint64_t> queries;
+};
+std::vector<FE> fibsq_trace(FE a1, uint32_t log_t);
+StarkProof prove_fibsq(FE a1, uint32_t log_t, uint32_t log_blowup, size_t num_queries, FriChannel& channel,
+                       FE offset = FE(FRI_GENERATOR), std::shared_ptr<Gpu> gpu = nullptr);
+// CP(x) from f(x), f(gx), f(g^2 x): what layer 0 must hold at a query.
+FE fibsq_composition_at(FE f0, FE f1, FE f2, FE x, const std::array<FE, 3>& alphas, FE a_last, uint32_t log_t);
+// Verifier of prove_fibsq's transcript: replays the channel, checks the
+// trace paths against the trace root, layer 0 against the composition at
+// every query, then every check of verify_fri.  Host-only.
+bool verify_fibsq(const std::vector<std::vector<uint8_t>>& messages, FE a_last, uint32_t log_t, uint32_t log_blowup,
+                  size_t num_queries, size_t n_layers, FE offset = FE(FRI_GENERATOR),
+                  const std::string& channel_state = "");
 
 // ---------------------------------------------------- polynomial layer (GPU)
 // evaluate() at every coset point (fri_commit.rs:78): the LDE.

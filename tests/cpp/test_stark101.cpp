@@ -42,6 +42,19 @@ struct GoldenTranscript {
     const char* channel_in;
     std::vector<const char*> messages_hex;
 };
+struct GoldenFibsq {
+    const char* name;
+    uint32_t a1;
+    uint32_t log_t, log_blowup;
+    size_t queries;
+    const char* channel_in;
+    uint32_t a_last;
+    size_t n_layers;
+    const char* channel_out;
+    size_t messages;
+    const char* proof_sha;
+    std::vector<const char*> messages_hex;   // full transcript (two cases only)
+};
 #include "golden_cases.inc"
 
 // ------------------------------------------------------------ tiny harness
@@ -267,6 +280,31 @@ TEST(cpu, verify_fri_rejects_tampering) {
     }
 }
 
+// ======================================================= verify_fibsq (host)
+TEST(cpu, verify_fibsq_accepts_and_rejects) {
+    int checked = 0;
+    for (const auto& c : FIBSQ) {
+        if (c.messages_hex.empty()) continue;
+        std::vector<std::vector<uint8_t>> good;
+        for (auto* h : c.messages_hex) good.push_back(bytes_of(h));
+        auto ok = [&](const std::vector<std::vector<uint8_t>>& m, uint64_t a_last) {
+            return verify_fibsq(m, FE(a_last), c.log_t, c.log_blowup, c.queries, c.n_layers, FE(FRI_GENERATOR),
+                                c.channel_in);
+        };
+        ASSERT_TRUE(ok(good, c.a_last));
+        ASSERT_TRUE(!ok(good, c.a_last + 1));                   // another public output
+        for (size_t i = 0; i < good.size(); i++) {
+            if (good[i].empty()) continue;
+            auto bad = good;
+            bad[i][bad[i].size() / 2] ^= 0x01;
+            ASSERT_TRUE(!ok(bad, c.a_last));
+        }
+        checked++;
+    }
+    ASSERT_EQ(checked, 2);
+    ASSERT_EQ(fibsq_trace(FE(3141592), 3)[7].value(), static_cast<uint64_t>(FIBSQ[0].a_last));
+}
+
 // ================================================================== GPU
 static Coset coset_of(const GoldenCase& c) { return Coset(FE(c.offset), omega(c.log_n), size_t{1} << c.log_n); }
 static Poly poly_of(const GoldenCase& c) {
@@ -372,6 +410,29 @@ TEST(gpu, reference_panics) {
     ASSERT_PANICS(interpolate(dom, std::vector<FE>(dom.size() - 1)));      // interpolation.rs:127
     ASSERT_PANICS(MerkleTree(std::vector<FE>{}));                          // merkle/mod.rs:25
     ASSERT_EQ(ch.proof.size(), 0u);                                        // nothing sent on failure
+}
+
+TEST(gpu, prove_fibsq_matches_golden) {
+    for (const auto& c : FIBSQ) {
+        FriChannel ch;
+        ch.state = c.channel_in;
+        StarkProof sp = prove_fibsq(FE(c.a1), c.log_t, c.log_blowup, c.queries, ch);
+        ASSERT_EQ(sp.a_last.value(), static_cast<uint64_t>(c.a_last));
+        ASSERT_EQ(sp.fri.n_layers(), c.n_layers);
+        ASSERT_EQ(ch.state, std::string(c.channel_out));
+        ASSERT_EQ(ch.proof.size(), c.messages);
+        ASSERT_EQ(transcript_sha(ch.proof, 0), std::string(c.proof_sha));
+        ASSERT_TRUE(verify_fibsq(ch.proof, sp.a_last, c.log_t, c.log_blowup, c.queries, sp.fri.n_layers(),
+                                 FE(FRI_GENERATOR), c.channel_in));
+    }
+    // configs[3] size: 2^16 rows, blowup 8, 3 queries; self-consistent + verified
+    FriChannel ch;
+    StarkProof sp = prove_fibsq(FE(3141592), 16, 3, 3, ch);
+    ASSERT_EQ(sp.fri.betas.size(), 17u);                         // deg CP = T = 2^16
+    ASSERT_TRUE(verify_fibsq(ch.proof, sp.a_last, 16, 3, 3, sp.fri.n_layers()));
+    auto bad = ch.proof;
+    bad[10][0] ^= 0x01;
+    ASSERT_TRUE(!verify_fibsq(bad, sp.a_last, 16, 3, 3, sp.fri.n_layers()));
 }
 
 int main(int argc, char** argv) {

@@ -37,6 +37,7 @@ def test_cpp_host_mirror_cpu():
     out = _run("cpu")
     assert "ok   cpu::channel_replays_golden_commits" in out
     assert "ok   cpu::verify_fri_rejects_tampering" in out
+    assert "ok   cpu::verify_fibsq_accepts_and_rejects" in out
 
 
 def test_host_library_exports_reference_api():
@@ -45,7 +46,8 @@ def test_host_library_exports_reference_api():
                           capture_output=True, text=True, check=True).stdout
     for name in ("stark101::fri_commit(", "stark101::decommit_fri(", "stark101::decommit_fri_layers(",
                  "stark101::verify_fri(", "stark101::MerkleTree::MerkleTree(", "stark101::interpolate(",
-                 "stark101::batch_inverse(", "stark101::evaluate_on_coset("):
+                 "stark101::batch_inverse(", "stark101::evaluate_on_coset(", "stark101::prove_fibsq(",
+                 "stark101::verify_fibsq("):
         assert name in syms, name
     needed = subprocess.run(["readelf", "-d", os.path.join(PKG, "lib", "libstark101.so")],
                             capture_output=True, text=True, check=True).stdout
@@ -57,3 +59,4 @@ def test_host_library_exports_reference_api():
 def test_cpp_host_mirror_gpu():
     out = _run("gpu")
     assert "ok   gpu::fri_commit_and_decommit_match_golden" in out
+    assert "ok   gpu::prove_fibsq_matches_golden" in out
