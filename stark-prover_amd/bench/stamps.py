@@ -15,15 +15,19 @@ ctx = fri_amd.Context(0, log_n)
 c = (np.arange(d, dtype=np.uint64) * 2654435761 % fri_amd.P).astype(np.uint32)
 for _ in range(3):
     res = ctx.commit(c, log_n)
-buf = (ctypes.c_uint64 * (33 * 24))()
-ctx._check(ctx.lib.fri_debug_stamps(ctx.h, buf, 33 * 24))
-a = np.frombuffer(buf, dtype=np.uint64).reshape(33, 24).astype(np.int64)
+buf = (ctypes.c_uint64 * (33 * 64))()
+ctx._check(ctx.lib.fri_debug_stamps(ctx.h, buf, 33 * 64))
+a = np.frombuffer(buf, dtype=np.uint64).reshape(33, 64).astype(np.int64)
 prev_end = 0
 for k in range(res.n_layers):
     row = a[k]
     t0 = row[0]
-    marks = [(i, (row[i] - t0) / 100.0) for i in range(1, 24) if row[i] > 0]
-    last = max(row[i] for i in range(24))
+    marks = [(i, (row[i] - t0) / 100.0) for i in range(1, 17) if row[i] > 0]
+    if row[17] and row[18] and row[19] > row[1]:
+        marks.append(("MHz", (row[18] - row[17]) / ((row[19] - row[1]) / 100.0)))
+    last = max(row[i] for i in list(range(17)) + [19])
     gap = (t0 - prev_end) / 100.0 if k else 0.0
     prev_end = last
     print(f"layer {k:2d} L={log_n - k:2d} since-prev-top={gap:6.1f}: " + " ".join(f"{i}:{us:.1f}" for i, us in marks))
+    nodes = [(row[25 + 2 * j] - row[24 + 2 * j]) / 1000.0 for j in range(18) if row[25 + 2 * j] > row[24 + 2 * j] > 0]
+    print("      node kcycles per level: " + " ".join(f"{c:.1f}" for c in nodes))

@@ -37,7 +37,7 @@ struct DevState {
     uint32_t forced_beta[MAXR];
     uint32_t roots[MAXR + 1][8];
 #ifdef FRI_STAMPS
-    uint64_t stamps[MAXR + 1][24];   // diagnostic build only: s_memrealtime (100 MHz) per phase
+    uint64_t stamps[MAXR + 1][64];   // diagnostic build only: s_memrealtime (100 MHz) per phase
 #endif
 };
 

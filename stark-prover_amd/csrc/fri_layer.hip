@@ -33,12 +33,17 @@ constexpr uint32_t INV2_M2 = 0x80000000u;   // Montgomery(2^-1) = 2^31 mod p
     do {                                                                                 \
         if (COMMIT && threadIdx.x == 0) t.st->stamps[t.k][(i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+#define TOP_CLK(i)                                                                               \
+    do {                                                                                           \
+        if (COMMIT && threadIdx.x == 0) t.st->stamps[t.k][(i)] = __builtin_amdgcn_s_memtime();     \
+    } while (0)
 #define TOP_STAMP_T(i, tid_)                                                                       \
     do {                                                                                           \
         if (COMMIT && threadIdx.x == (tid_)) t.st->stamps[t.k][(i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define TOP_STAMP(i) do {} while (0)
+#define TOP_CLK(i) do {} while (0)
 #define TOP_STAMP_T(i, tid_) do {} while (0)
 #endif
 
@@ -402,6 +407,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     const uint32_t L = t.L;
     const uint32_t N = 1u << (L - l);
     const uint32_t tid = threadIdx.x;
+
     const bool chan_wave = COMMIT && tid >= 448;
     DevState* st = t.st;
     uint32_t cs[8], X[8];
@@ -467,6 +473,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     uint32_t fv = 0;                               // fri_commit.rs:109-113
     if (chan_wave && is_final && deg == 0) fv = (t.k == 0 ? t.coef_in : t.coef_out)[0];
     TOP_STAMP(1);
+    TOP_CLK(17);
     // iterations: the levels, then the channel jobs still left after them
     const uint32_t nlev = L - l;
     uint32_t total = nlev;
@@ -487,7 +494,13 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
                 Dg a, b, o;
                 dg_lds_load(A + 4 * q, a);
                 dg_lds_load(A + 4 * q + 2, b);
+#ifdef FRI_STAMPS
+                if (it < 18 && q == 0) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); TOP_CLK(24 + 2 * it); }
+#endif
                 cnode(a, b, o);
+#ifdef FRI_STAMPS
+                if (it < 18 && q == 0) TOP_CLK(25 + 2 * it);
+#endif
                 dg_lds_store(B + 2 * q, o);
                 dg_store(out + 8 * q, o);
             }
@@ -502,6 +515,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         if (level) {
             uint4* tmp = A; A = B; B = tmp;
             if (it < 11) TOP_STAMP(2 + it);
+            if (it + 1 == nlev) { TOP_CLK(18); TOP_STAMP(19); }
         }
     }
     if (!COMMIT || tid != 448) return;
