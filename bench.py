@@ -94,6 +94,8 @@ def main():
                     help="sharded data path: the library's RCCL communicator, or host-staged gloo (rehearsal only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the side measurements (PCIe-inclusive, serving, prover): A/B timing runs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -270,7 +272,7 @@ def main():
 
     # PCIe-inclusive rate (host coefficients in, result out): never `value`
     pcie = None
-    if world == 1:
+    if world == 1 and not args.no_extras:
         k = max(3, min(args.steps, 10))
         t0 = time.perf_counter()
         for _ in range(k):
@@ -282,7 +284,7 @@ def main():
     # -> iNTT -> coset LDE 2^19 -> Merkle commit, device-resident (reported
     # beside the metric, never `value`).
     trace_stage = None
-    if world == 1 and log_n >= 19:
+    if world == 1 and log_n >= 19 and not args.no_extras:
         tr = _coeffs(7, 1 << 16, fri_amd.P)
         ctx.trace_commit(tr, 3)
         k = 10
@@ -298,7 +300,7 @@ def main():
     # The tree tops of one commit (one workgroup on the serial Fiat-Shamir
     # chain) overlap the leaf hashing of the others.  Beside `value`, never it.
     concurrent = None
-    if world == 1 and mode == "single" and log_n >= 20:
+    if world == 1 and mode == "single" and log_n >= 20 and not args.no_extras:
         concurrent = _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C=3, steps=max(5, args.steps // 2))
 
     # Whole prover slice, BASELINE configs[3]: STARK-101 FibonacciSq trace of
@@ -306,7 +308,7 @@ def main():
     # FRI commit -> 3 queries (trace + FRI decommitments); host trace in,
     # transcript out.  Reported beside the metric, never `value`.
     prover = None
-    if world == 1 and log_n >= 19:
+    if world == 1 and log_n >= 19 and not args.no_extras:
         prover = _prover_stage(ctx, fri_amd, with_cpu=(rank == 0 and not args.no_cpu_baseline))
 
     cpu = None

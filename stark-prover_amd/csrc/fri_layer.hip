@@ -21,6 +21,7 @@
 // levels +3/+4 pair through LDS.  Loads/stores of values are 16 B per lane.
 #include "fri_internal.hpp"
 #include "sha256_fast.hpp"
+#include "sha256_quad.hpp"
 
 namespace fri {
 
@@ -75,6 +76,26 @@ __device__ __forceinline__ void hleaf(uint32_t v, Dg& o) { shaf::leaf(v, o.w); }
 // compact (looped) forms for the latency-bound mid / top kernels
 __device__ __forceinline__ void cnode(const Dg& l, const Dg& r, Dg& o) { shaf::node_compact(l.w, r.w, o.w); }
 __device__ __forceinline__ void cleaf(uint32_t v, Dg& o) { shaf::leaf_compact(v, o.w); }
+
+// One node per quad of lanes (sha256_quad.hpp) for the narrow, latency-bound
+// levels: thread `tid` < 4*cnt hashes node tid/4; lane 0 of the quad writes
+// digest words 4..7, lane 1 words 0..3 (LDS for the next level, and HBM).
+__device__ __forceinline__ void quad_level(const uint4* A, uint4* B, uint32_t* out, uint32_t tid, uint32_t cnt,
+                                           const shaq::Role& R) {
+    if (tid >= 4 * cnt) return;
+    const uint32_t q = tid >> 2, role = tid & 3u;
+    Dg a, b;
+    dg_lds_load(A + 4 * q, a);
+    dg_lds_load(A + 4 * q + 2, b);
+    uint32_t o[4];
+    shaq::node(a.w, b.w, o, R);
+    if (role < 2) {
+        const uint32_t half = role == 0 ? 1u : 0u;
+        const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
+        B[2 * q + half] = v;
+        reinterpret_cast<uint4*>(out + 8 * q)[half] = v;
+    }
+}
 
 // Barrier that waits only for this wave's LDS traffic: HIP's __syncthreads()
 // also drains vmcnt, i.e. waits ~1 us for the level's global digest stores,
@@ -275,17 +296,21 @@ __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L
     dg_lds_store(A + 2 * (t + NIN / 2), d1);
     if (mx_in) reduce_mx(mx_in, mx_out, blockIdx.x, R);
     lds_barrier();
+    const shaq::Role qr = shaq::role_of(t);
     uint32_t cnt = NIN;
 #pragma unroll 1
     for (uint32_t j = 1; j <= 4; j++) {
         cnt >>= 1;
-        if (t < cnt) {
+        uint32_t* out = tree + 8 * (level_offset(L, l + j) + (base >> j));
+        if (4 * cnt <= NIN / 2) {
+            quad_level(A, B, out, t, cnt, qr);         // narrow: latency-bound
+        } else if (t < cnt) {
             Dg a, b, o;
             dg_lds_load(A + 4 * t, a);
             dg_lds_load(A + 4 * t + 2, b);
             hnode(a, b, o);
             dg_lds_store(B + 2 * t, o);
-            dg_store(tree + 8 * (level_offset(L, l + j) + (base >> j) + t), o);
+            dg_store(out + 8 * t, o);
         }
         lds_barrier();
         uint4* tmp = A; A = B; B = tmp;
@@ -482,6 +507,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         const uint32_t pre_in_levels = min(n_pre, min(nlev, 8u));   // levels with <= 128 nodes
         total += (n_pre - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
     }
+    const shaq::Role R = shaq::role_of(tid);
     uint32_t cnt = N;
 #pragma unroll 1
     for (uint32_t it = 0; it < total; it++) {
@@ -489,20 +515,30 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         if (level) {
             cnt >>= 1;
             uint32_t* out = tr + 8 * level_offset(L, l + 1 + it);
+            if (cnt <= 64) {                    // waves 0-3, one per SIMD (wave 7: channel)
+#ifdef FRI_STAMPS
+                if (it < 18 && tid == 0) TOP_CLK(24 + 2 * it);
+#endif
+                quad_level(A, B, out, tid, cnt, R);
+#ifdef FRI_STAMPS
+                if (it < 18 && tid == 0) TOP_CLK(25 + 2 * it);
+#endif
+            } else {
 #pragma unroll 1
-            for (uint32_t q = tid; q < cnt; q += blockDim.x) {
-                Dg a, b, o;
-                dg_lds_load(A + 4 * q, a);
-                dg_lds_load(A + 4 * q + 2, b);
+                for (uint32_t q = tid; q < cnt; q += blockDim.x) {
+                    Dg a, b, o;
+                    dg_lds_load(A + 4 * q, a);
+                    dg_lds_load(A + 4 * q + 2, b);
 #ifdef FRI_STAMPS
-                if (it < 18 && q == 0) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); TOP_CLK(24 + 2 * it); }
+                    if (it < 18 && q == 0) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); TOP_CLK(24 + 2 * it); }
 #endif
-                cnode(a, b, o);
+                    cnode(a, b, o);
 #ifdef FRI_STAMPS
-                if (it < 18 && q == 0) TOP_CLK(25 + 2 * it);
+                    if (it < 18 && q == 0) TOP_CLK(25 + 2 * it);
 #endif
-                dg_lds_store(B + 2 * q, o);
-                dg_store(out + 8 * q, o);
+                    dg_lds_store(B + 2 * q, o);
+                    dg_store(out + 8 * q, o);
+                }
             }
         }
         // channel job: during the narrow levels (SIMD 3 idle) only the

@@ -1,0 +1,141 @@
+// sha256_quad.hpp — SHA-256 Merkle node for the latency-bound tree levels,
+// one node per QUAD of lanes (gfx950, device only).
+//
+// A lone wave issues about one VALU instruction per 4-5 cycles while a
+// dependent instruction waits ~8, so a node hash on the
+// serial tree top is bound by its instruction COUNT.  A SHA-256 round has
+// two halves: the e-path (Sigma1, Ch, T1, e' = d + T1) and the a-path
+// (Sigma0, Maj, a' = T1 + T2).  Here lane 0 of a quad runs the e-path and
+// lane 1 the a-path with the SAME instructions (per-lane rotation amounts
+// and masks); lanes 2-3 hold zeros.  One DPP quad_perm add per round swaps
+// the halves' results:
+//     E: V = Sigma1(e) + Ch(e,f,g) + h + K + W = T1      exports T1
+//     A: V = Sigma0(a) + Maj(a,b,c)            = T2      exports d
+//     E: e' = V + d (from A)      A: a' = V + T1 (from E)
+// 11 instructions per round instead of 14.  The shift registers (e,f,g,h)
+// and (a,b,c,d) never move between lanes, so the chaining value and the
+// digest stay split: E holds words 4..7, A holds words 0..3.
+//
+// The message schedule is split the same way: E computes sigma1(W[t-2]),
+// A computes sigma0(W[t-15]) (per-lane operand select, rotation and shift
+// amounts) and the two halves meet through one more DPP add: 7 instructions
+// per word instead of 10.  Both lanes keep the whole schedule.
+//
+// Measured (stark-prover_amd/bench/quad_micro.hip, one wave, dependent
+// chain): 9.0 K cycles per node against 9.9 K for the compact per-lane node;
+// used for the tree levels of <= 64 nodes in k_tree_top and k_tree_mid
+// (5.19 -> 5.02 ms per 2^24 commit, tools/abn.sh).  The DPP add must carry
+// bound_ctrl so the compiler fuses it (v_add_u32_dpp) instead of emitting a
+// separate v_mov_b32_dpp.
+#pragma once
+#include <stdint.h>
+#include "sha256_fast.hpp"
+
+namespace fri {
+namespace shaq {
+
+// quad_perm [1,0,2,3]: lane 0 <-> lane 1, lanes 2 and 3 read themselves
+constexpr int SWAP01 = 1 | (0 << 2) | (2 << 4) | (3 << 6);
+
+__device__ __forceinline__ uint32_t swap01(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, SWAP01, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t rot(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+#define bop(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))
+
+// Per-lane role constants of a quad.
+struct Role {
+    uint32_t r1, r2, r3;    // round rotations: E 6,11,25 (Sigma1)  A 2,13,22 (Sigma0)
+    uint32_t m;             // sel mask:  E 0 (sel = ~e -> Ch)     A ~0 (sel = a^b -> Maj)
+    uint32_t me;            // ~0 on E only
+    uint32_t q1, q2, q3;    // schedule: E sigma1 (17,19,>>10), A sigma0 (7,18,>>3)
+    uint32_t is_a;          // ~0 on A only (schedule operand select)
+    uint32_t iv[4];         // initial chaining words of this lane's half
+};
+
+__device__ __forceinline__ Role role_of(uint32_t lane) {
+    Role r{};
+    const uint32_t q = lane & 3u;
+    const uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                            0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    if (q == 0) {
+        r.r1 = 6; r.r2 = 11; r.r3 = 25; r.m = 0u; r.me = ~0u;
+        r.q1 = 17; r.q2 = 19; r.q3 = 10; r.is_a = 0u;
+        for (int i = 0; i < 4; i++) r.iv[i] = IV[4 + i];
+    } else if (q == 1) {
+        r.r1 = 2; r.r2 = 13; r.r3 = 22; r.m = ~0u; r.me = 0u;
+        r.q1 = 7; r.q2 = 18; r.q3 = 3; r.is_a = ~0u;
+        for (int i = 0; i < 4; i++) r.iv[i] = IV[i];
+    } else {
+        r.r1 = 0; r.r2 = 0; r.r3 = 0; r.m = 0u; r.me = 0u;
+        r.q1 = 0; r.q2 = 0; r.q3 = 0; r.is_a = 0u;
+        for (int i = 0; i < 4; i++) r.iv[i] = 0u;
+    }
+    return r;
+}
+
+// One round on this lane's half (x0..x3 = e,f,g,h on E; a,b,c,d on A).
+#define SHAQ_R(kw)                                                                   \
+    {                                                                                \
+        const uint32_t _S = bop(rot(x0, R.r1), rot(x0, R.r2), rot(x0, R.r3), 0x96);  \
+        const uint32_t _sel = bop(x0, x1, R.m, 0x2D);   /* x0 ^ (x1 & m) ^ ~m */     \
+        const uint32_t _F = bop(_sel, x2, x1, 0xCA);    /* sel ? x2 : x1 */          \
+        const uint32_t _hk = (x3 + (kw)) & R.me;                                     \
+        const uint32_t _V = _S + _F + _hk;                                           \
+        const uint32_t _Z = bop(R.me, _V, x3, 0xCA);    /* E: T1, A: d */            \
+        const uint32_t _n = _V + swap01(_Z);                                         \
+        x3 = x2; x2 = x1; x1 = x0; x0 = _n;                                          \
+    }
+
+// Split schedule word: w[i] (= W[t-16]) <- W[t]
+#define SHAQ_W(i)                                                                            \
+    {                                                                                        \
+        const uint32_t _x = bop(R.is_a, w[((i) + 1) & 15], w[((i) + 14) & 15], 0xCA);        \
+        const uint32_t _s = bop(rot(_x, R.q1), rot(_x, R.q2), _x >> R.q3, 0x96);             \
+        w[i] = w[i] + w[((i) + 9) & 15] + _s + swap01(_s);                                   \
+    }
+
+// Block on a register message w[16] (consumed), looped 16 rounds at a time.
+__device__ __forceinline__ void compress(uint32_t st[4], uint32_t w[16], const Role& R) {
+    uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+#pragma unroll
+    for (int i = 0; i < 16; i++) SHAQ_R(w[i] + shaf::KTAB[i]);
+#pragma unroll 1
+    for (int r = 1; r < 4; r++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            SHAQ_W(i);
+            SHAQ_R(w[i] + shaf::KTAB[16 * r + i]);
+        }
+    }
+    st[0] += x0; st[1] += x1; st[2] += x2; st[3] += x3;
+}
+// Block with a constant K+W table (the padding block of a 64-byte message).
+__device__ __forceinline__ void compress_kw(uint32_t st[4], const uint32_t* kw, const Role& R) {
+    uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+#pragma unroll 1
+    for (int r = 0; r < 4; r++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) SHAQ_R(kw[16 * r + i]);
+    }
+    st[0] += x0; st[1] += x1; st[2] += x2; st[3] += x3;
+}
+#undef SHAQ_R
+#undef SHAQ_W
+#undef bop
+
+// Node hash SHA256(l || r): every lane of the quad passes the same 16
+// message words; out = this lane's half of the digest (E: words 4..7,
+// A: words 0..3, other lanes: garbage).
+__device__ __forceinline__ void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[4], const Role& R) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) { w[i] = l[i]; w[8 + i] = r[i]; }
+#pragma unroll
+    for (int i = 0; i < 4; i++) out[i] = R.iv[i];
+    compress(out, w, R);
+    compress_kw(out, shaf::PAD_KW_C.kw, R);
+}
+
+}  // namespace shaq
+}  // namespace fri
