@@ -30,10 +30,10 @@ __global__ void k_std(const uint32_t* in, uint32_t* out, int reps, unsigned long
 }
 
 __global__ void k_quad(const uint32_t* in, uint32_t* out, int reps, unsigned long long* t) {
-    __shared__ uint32_t dig[16 * 16];
-    const int lane = threadIdx.x, q = lane >> 2, role = lane & 3;
+    __shared__ uint32_t dig[32 * 16];
+    const int lane = threadIdx.x, q = lane >> 1, role = lane & 1;
     const shaq::Role R = shaq::role_of(lane);
-    if (role == 0) for (int i = 0; i < 16; i++) dig[q * 16 + i] = in[q * 16 + i];
+    if (role == 0) for (int i = 0; i < 16; i++) dig[q * 16 + i] = in[(q & 15) * 16 + i];
     __syncthreads();
     unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
     for (int k = 0; k < reps; k++) {
@@ -42,7 +42,7 @@ __global__ void k_quad(const uint32_t* in, uint32_t* out, int reps, unsigned lon
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         shaq::node(l, r, o, R);
         // E writes words 4..7 (and r ^ o), A writes words 0..3
-        if (role < 2) {
+        {
             const int base = role == 0 ? 4 : 0;
             for (int i = 0; i < 4; i++) { dig[q * 16 + base + i] = o[i]; dig[q * 16 + 8 + base + i] = r[base + i] ^ o[i]; }
         }

@@ -77,24 +77,21 @@ __device__ __forceinline__ void hleaf(uint32_t v, Dg& o) { shaf::leaf(v, o.w); }
 __device__ __forceinline__ void cnode(const Dg& l, const Dg& r, Dg& o) { shaf::node_compact(l.w, r.w, o.w); }
 __device__ __forceinline__ void cleaf(uint32_t v, Dg& o) { shaf::leaf_compact(v, o.w); }
 
-// One node per quad of lanes (sha256_quad.hpp) for the narrow, latency-bound
-// levels: thread `tid` < 4*cnt hashes node tid/4; lane 0 of the quad writes
-// digest words 4..7, lane 1 words 0..3 (LDS for the next level, and HBM).
-__device__ __forceinline__ void quad_level(const uint4* A, uint4* B, uint32_t* out, uint32_t tid, uint32_t cnt,
+// One node per pair of lanes (sha256_quad.hpp) for the narrow, latency-bound
+// levels: thread `tid` < 2*cnt hashes node tid/2; the even lane writes
+// digest words 4..7, the odd lane words 0..3 (LDS for the next level, HBM).
+__device__ __forceinline__ void pair_level(const uint4* A, uint4* B, uint32_t* out, uint32_t tid, uint32_t cnt,
                                            const shaq::Role& R) {
-    if (tid >= 4 * cnt) return;
-    const uint32_t q = tid >> 2, role = tid & 3u;
+    if (tid >= 2 * cnt) return;
+    const uint32_t q = tid >> 1, half = (tid & 1u) ^ 1u;
     Dg a, b;
     dg_lds_load(A + 4 * q, a);
     dg_lds_load(A + 4 * q + 2, b);
     uint32_t o[4];
     shaq::node(a.w, b.w, o, R);
-    if (role < 2) {
-        const uint32_t half = role == 0 ? 1u : 0u;
-        const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
-        B[2 * q + half] = v;
-        reinterpret_cast<uint4*>(out + 8 * q)[half] = v;
-    }
+    const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
+    B[2 * q + half] = v;
+    reinterpret_cast<uint4*>(out + 8 * q)[half] = v;
 }
 
 // Barrier that waits only for this wave's LDS traffic: HIP's __syncthreads()
@@ -302,8 +299,8 @@ __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L
     for (uint32_t j = 1; j <= 4; j++) {
         cnt >>= 1;
         uint32_t* out = tree + 8 * (level_offset(L, l + j) + (base >> j));
-        if (4 * cnt <= NIN / 2) {
-            quad_level(A, B, out, t, cnt, qr);         // narrow: latency-bound
+        if (2 * cnt <= NIN / 2) {
+            pair_level(A, B, out, t, cnt, qr);         // narrow: latency-bound
         } else if (t < cnt) {
             Dg a, b, o;
             dg_lds_load(A + 4 * t, a);
@@ -515,11 +512,11 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         if (level) {
             cnt >>= 1;
             uint32_t* out = tr + 8 * level_offset(L, l + 1 + it);
-            if (cnt <= 64) {                    // waves 0-3, one per SIMD (wave 7: channel)
+            if (cnt <= 128) {                   // waves 0-3, one per SIMD (wave 7: channel)
 #ifdef FRI_STAMPS
                 if (it < 18 && tid == 0) TOP_CLK(24 + 2 * it);
 #endif
-                quad_level(A, B, out, tid, cnt, R);
+                pair_level(A, B, out, tid, cnt, R);
 #ifdef FRI_STAMPS
                 if (it < 18 && tid == 0) TOP_CLK(25 + 2 * it);
 #endif

@@ -1,14 +1,14 @@
 // sha256_quad.hpp — SHA-256 Merkle node for the latency-bound tree levels,
-// one node per QUAD of lanes (gfx950, device only).
+// one node per PAIR of lanes (gfx950, device only).
 //
 // A lone wave issues about one VALU instruction per 4-5 cycles while a
 // dependent instruction waits ~8, so a node hash on the
 // serial tree top is bound by its instruction COUNT.  A SHA-256 round has
 // two halves: the e-path (Sigma1, Ch, T1, e' = d + T1) and the a-path
-// (Sigma0, Maj, a' = T1 + T2).  Here lane 0 of a quad runs the e-path and
-// lane 1 the a-path with the SAME instructions (per-lane rotation amounts
-// and masks); lanes 2-3 hold zeros.  One DPP quad_perm add per round swaps
-// the halves' results:
+// (Sigma0, Maj, a' = T1 + T2).  Here the even lane of a pair runs the e-path
+// and the odd lane the a-path with the SAME instructions (per-lane rotation
+// amounts and masks).  One DPP quad_perm add per round swaps the halves'
+// results:
 //     E: V = Sigma1(e) + Ch(e,f,g) + h + K + W = T1      exports T1
 //     A: V = Sigma0(a) + Maj(a,b,c)            = T2      exports d
 //     E: e' = V + d (from A)      A: a' = V + T1 (from E)
@@ -34,8 +34,8 @@
 namespace fri {
 namespace shaq {
 
-// quad_perm [1,0,2,3]: lane 0 <-> lane 1, lanes 2 and 3 read themselves
-constexpr int SWAP01 = 1 | (0 << 2) | (2 << 4) | (3 << 6);
+// quad_perm [1,0,3,2]: lane 2k <-> lane 2k+1
+constexpr int SWAP01 = 1 | (0 << 2) | (3 << 4) | (2 << 6);
 
 __device__ __forceinline__ uint32_t swap01(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, SWAP01, 0xF, 0xF, true);
@@ -43,7 +43,7 @@ __device__ __forceinline__ uint32_t swap01(uint32_t v) {
 __device__ __forceinline__ uint32_t rot(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
 #define bop(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))
 
-// Per-lane role constants of a quad.
+// Per-lane role constants of a pair.
 struct Role {
     uint32_t r1, r2, r3;    // round rotations: E 6,11,25 (Sigma1)  A 2,13,22 (Sigma0)
     uint32_t m;             // sel mask:  E 0 (sel = ~e -> Ch)     A ~0 (sel = a^b -> Maj)
@@ -55,21 +55,16 @@ struct Role {
 
 __device__ __forceinline__ Role role_of(uint32_t lane) {
     Role r{};
-    const uint32_t q = lane & 3u;
     const uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                             0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-    if (q == 0) {
+    if ((lane & 1u) == 0) {
         r.r1 = 6; r.r2 = 11; r.r3 = 25; r.m = 0u; r.me = ~0u;
         r.q1 = 17; r.q2 = 19; r.q3 = 10; r.is_a = 0u;
         for (int i = 0; i < 4; i++) r.iv[i] = IV[4 + i];
-    } else if (q == 1) {
+    } else {
         r.r1 = 2; r.r2 = 13; r.r3 = 22; r.m = ~0u; r.me = 0u;
         r.q1 = 7; r.q2 = 18; r.q3 = 3; r.is_a = ~0u;
         for (int i = 0; i < 4; i++) r.iv[i] = IV[i];
-    } else {
-        r.r1 = 0; r.r2 = 0; r.r3 = 0; r.m = 0u; r.me = 0u;
-        r.q1 = 0; r.q2 = 0; r.q3 = 0; r.is_a = 0u;
-        for (int i = 0; i < 4; i++) r.iv[i] = 0u;
     }
     return r;
 }
@@ -124,9 +119,9 @@ __device__ __forceinline__ void compress_kw(uint32_t st[4], const uint32_t* kw, 
 #undef SHAQ_W
 #undef bop
 
-// Node hash SHA256(l || r): every lane of the quad passes the same 16
-// message words; out = this lane's half of the digest (E: words 4..7,
-// A: words 0..3, other lanes: garbage).
+// Node hash SHA256(l || r): both lanes of the pair pass the same 16
+// message words; out = this lane's half of the digest (even lane: words
+// 4..7, odd lane: words 0..3).
 __device__ __forceinline__ void node(const uint32_t l[8], const uint32_t r[8], uint32_t out[4], const Role& R) {
     uint32_t w[16];
 #pragma unroll
