@@ -1,6 +1,6 @@
 """Per-dispatch timeline of one FRI commit from a rocprofv3 kernel trace.
 
-Usage: python tools/timeline.py <kernel_trace.csv> [commit_index_from_end=1]
+Usage: python tools/timeline.py <kernel_trace.csv> [commit_index_from_end=1] [min_layer0_us=0]
 
 A commit starts at its first k_ntt_pass dispatch; prints, for the chosen
 commit, every kernel's start offset, duration and the idle gap before it, plus
@@ -27,7 +27,9 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     rows.sort()
     first = [i for i, r in enumerate(rows) if r[2].startswith("k_ntt_pass") and r[2].split(",")[2].strip() == "true"]
-    l0 = [i for i, r in enumerate(rows) if r[2].startswith("k_layer_leaf<false, true>")]
+    min_us = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0      # layer-0 leaf duration filter
+    l0 = [i for i, r in enumerate(rows)
+          if r[2].startswith("k_layer_leaf<false, true>") and (r[1] - r[0]) / 1e3 >= min_us]
     anchor = l0[-which]
     lo = max(i for i in first if i < anchor)
     later = [i for i in first if i > anchor]
