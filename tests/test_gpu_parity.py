@@ -470,3 +470,43 @@ def test_verify_fri_on_device_transcript(ctx):
     bad = list(ch.proof)
     bad[-3] = bytes([bad[-3][0] ^ 1]) + bad[-3][1:]          # a sibling value of the last query
     assert not fri_amd.verify_fri(bad, log_n, proof.n_layers, 8, (1 << log_n) - 1)
+
+
+def test_concurrent_contexts_match_oracle(corc, oracle):
+    """Serving pattern (INTEGRATION.md "Threading and serving"): one context
+    per host thread on one GPU, commits in flight together, every transcript
+    bit-exact against the C oracle."""
+    import threading
+
+    import fri_amd
+    log_n, C, reps = 18, 3, 4
+    d = (1 << log_n) // 8
+    polys = [np.array(oracle.splitmix64_field(900 + c, d), dtype=np.uint64) for c in range(C)]
+    want = []
+    for p in polys:
+        cs, pc = c_u64(p)
+        och = oracle.OrcChannel()
+        corc.orc_channel_init(ctypes.byref(och))
+        ores = oracle.OrcFriResult()
+        assert corc.orc_fri_commit_fast(pc, d, log_n, 5, 5, P, ctypes.byref(och), None, ctypes.byref(ores),
+                                        None, None) == 0
+        want.append(([bytes(ores.roots[k]) for k in range(ores.n_layers)],
+                     [int(ores.betas[k]) for k in range(ores.n_rounds)], int(ores.final_value)))
+    ctxs = [fri_amd.Context(0, log_n) for _ in range(C)]
+    got = [[] for _ in range(C)]
+
+    def run(c):
+        for _ in range(reps):
+            got[c].append(ctxs[c].commit(polys[c], log_n))
+
+    th = [threading.Thread(target=run, args=(c,)) for c in range(C)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for c in range(C):
+        assert len(got[c]) == reps
+        for r in got[c]:
+            assert ([bytes(r.roots[k]) for k in range(r.n_layers)], [int(r.betas[k]) for k in range(r.n_rounds)],
+                    int(r.final_value)) == want[c]
+        ctxs[c].close()
