@@ -34,6 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "stark-prover_amd", "python"))
 METRIC = "FRI commit field-elems/sec at codeword 2^24; achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TOPS = 78.6            # 256 CU x 128 int32 lane-ops/clk x 2.4 GHz
+VALU_MEASURED_TOPS = 64.0        # full-rate v_xor/v_bitop3 streams over the whole chip (valu_cal.hip, lone_wave.hip)
 DOMINANT = "merkle_layer0_leaf"  # dominant kernel class (DESIGN.md "Roofline")
 
 
@@ -254,7 +255,9 @@ def main():
             roofline["valu"] = {"issue_units_per_launch": units,
                                 "achieved_T_units_s": round(units / (avg_ms * 1e-3) / 1e12, 2),
                                 "peak_T_units_s": VALU_PEAK_TOPS,
-                                "frac": round(units / (avg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)}
+                                "frac": round(units / (avg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
+                                "measured_ceiling_T_units_s": VALU_MEASURED_TOPS,
+                                "frac_of_measured_ceiling": round(units / (avg_ms * 1e-3) / 1e12 / VALU_MEASURED_TOPS, 4)}
         breakdown = {}
         for cls in ("lde", "alltoall", "merkle_layer0_leaf", "layer0", "layers", "gather"):
             cms, cl, _ = ctx.profile(cls)
