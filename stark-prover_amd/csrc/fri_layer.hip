@@ -280,23 +280,29 @@ template <uint32_t NIN>
 __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st,
                                                       int gate, const int32_t* mx_in, int32_t* mx_out, uint32_t R) {
     if (st && gate >= 0 && !st->active[gate]) return;
-    __shared__ uint4 lds[2 * NIN + NIN];
+    // level 1 reads its two inputs straight from HBM (64 contiguous bytes per
+    // thread), so LDS holds only levels 1.. (NIN/2 + NIN/4 digests): more
+    // workgroups per CU for the wide instance
+    __shared__ uint4 lds[NIN + NIN / 2];
     uint4* A = lds;
-    uint4* B = lds + 2 * NIN;
+    uint4* B = lds + NIN;
     const uint32_t t = threadIdx.x;
     const size_t base = (size_t)blockIdx.x * NIN;
     const uint32_t* in = tree + 8 * level_offset(L, l);
-    Dg d0, d1;
-    dg_load(in + 8 * (base + t), d0);
-    dg_load(in + 8 * (base + t + NIN / 2), d1);
-    dg_lds_store(A + 2 * t, d0);
-    dg_lds_store(A + 2 * (t + NIN / 2), d1);
-    if (mx_in) reduce_mx(mx_in, mx_out, blockIdx.x, R);
+    {
+        Dg a, b, o;
+        dg_load(in + 8 * (base + 2 * t), a);
+        dg_load(in + 8 * (base + 2 * t + 1), b);
+        if (mx_in) reduce_mx(mx_in, mx_out, blockIdx.x, R);
+        hnode(a, b, o);
+        dg_lds_store(A + 2 * t, o);
+        dg_store(tree + 8 * (level_offset(L, l + 1) + (base >> 1) + t), o);
+    }
     lds_barrier();
     const shaq::Role qr = shaq::role_of(t);
-    uint32_t cnt = NIN;
+    uint32_t cnt = NIN / 2;
 #pragma unroll 1
-    for (uint32_t j = 1; j <= 4; j++) {
+    for (uint32_t j = 2; j <= 4; j++) {
         cnt >>= 1;
         uint32_t* out = tree + 8 * (level_offset(L, l + j) + (base >> j));
         if (2 * cnt <= NIN / 2) {
