@@ -25,6 +25,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -406,6 +407,16 @@ def _prover_stage(ctx, fri_amd, with_cpu, log_t=16, log_b=3, queries=3, a1=31415
            "what": f"STARK-101 FibonacciSq prover: trace 2^{log_t} -> LDE 2^{log_t + log_b} + Merkle -> alphas -> "
                    f"composition polynomial -> FRI commit ({len(pr.fri.roots)} layers) -> {queries} queries; "
                    f"host trace in, transcript out (BASELINE configs[3])"}
+    # the same proof through the C++ host mirror (no interpreter in the query
+    # loop), when stark-prover_amd/build/prover_native is built
+    exe = os.path.join(ROOT, "stark-prover_amd", "build", "prover_native")
+    if os.path.exists(exe):
+        try:
+            r = subprocess.run([exe, str(log_t), str(log_b), str(queries), "10"], capture_output=True, text=True,
+                               timeout=120)
+            out["native_cpp"] = json.loads(r.stdout.strip().splitlines()[-1])
+        except Exception as e:  # noqa: BLE001
+            out["native_cpp"] = {"error": str(e)}
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         try:

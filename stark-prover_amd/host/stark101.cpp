@@ -8,8 +8,13 @@
 #include <functional>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
+#if defined(__x86_64__)
+#include <cpuid.h>
+#include <immintrin.h>
+#endif
 
 namespace stark101 {
 
@@ -27,30 +32,91 @@ constexpr uint32_t K256[64] = {
 
 inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-void compress(uint32_t h[8], const uint8_t blk[64]) {
-    uint32_t w[64];
-    for (int i = 0; i < 16; i++)
-        w[i] = (uint32_t)blk[4 * i] << 24 | (uint32_t)blk[4 * i + 1] << 16 | (uint32_t)blk[4 * i + 2] << 8 | blk[4 * i + 3];
-    for (int i = 16; i < 64; i++) {
-        uint32_t s0 = rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
-        uint32_t s1 = rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
-        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+void compress_scalar(uint32_t h[8], const uint8_t* data, size_t nblocks) {
+    for (; nblocks; nblocks--, data += 64) {
+        uint32_t w[64];
+        for (int i = 0; i < 16; i++)
+            w[i] = (uint32_t)data[4 * i] << 24 | (uint32_t)data[4 * i + 1] << 16 | (uint32_t)data[4 * i + 2] << 8 |
+                   data[4 * i + 3];
+        for (int i = 16; i < 64; i++) {
+            uint32_t s0 = rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
+            uint32_t s1 = rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
+            w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+        }
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
+        for (int i = 0; i < 64; i++) {
+            uint32_t t1 = k + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + K256[i] + w[i];
+            uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+            k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
     }
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
-    for (int i = 0; i < 64; i++) {
-        uint32_t t1 = k + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + K256[i] + w[i];
-        uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
-        k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+}
+
+#if defined(__x86_64__)
+// x86 SHA extensions: the transcript hashes ~3000 blocks per STARK-101 proof
+// (hex-encoded authentication paths), which dominates the host side of
+// prove/verify.  State kept as the instructions want it: ABEF = {F,E,B,A},
+// CDGH = {H,G,D,C} (dword 0 first).  Each 4-round group: W+K, two
+// sha256rnds2 (rounds 4g, 4g+1 from dwords 0-1, 4g+2, 4g+3 from 2-3); the
+// schedule W[t] = s1(W[t-2]) + W[t-7] + s0(W[t-15]) + W[t-16] is msg1 (adds
+// s0) + the W[t-7] lane window + msg2 (adds s1 with its in-vector chain).
+__attribute__((target("sha,sse4.1,ssse3"))) void compress_shani(uint32_t h[8], const uint8_t* data, size_t nblocks) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    const __m128i abcd = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(h)), 0xB1);      // B,A,D,C
+    const __m128i efgh = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(h + 4)), 0x1B);  // H,G,F,E
+    __m128i abef = _mm_alignr_epi8(abcd, efgh, 8);     // F,E,B,A
+    __m128i cdgh = _mm_blend_epi16(efgh, abcd, 0xF0);  // H,G,D,C
+    for (; nblocks; nblocks--, data += 64) {
+        const __m128i abef0 = abef, cdgh0 = cdgh;
+        __m128i m[4];
+        for (int j = 0; j < 4; j++)
+            m[j] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(data + 16 * j)), bswap);
+        for (int g = 0; g < 16; g++) {
+            if (g >= 4) {
+                __m128i x = _mm_sha256msg1_epu32(m[g & 3], m[(g + 1) & 3]);
+                x = _mm_add_epi32(x, _mm_alignr_epi8(m[(g + 3) & 3], m[(g + 2) & 3], 4));
+                m[g & 3] = _mm_sha256msg2_epu32(x, m[(g + 3) & 3]);
+            }
+            __m128i wk = _mm_add_epi32(m[g & 3], _mm_loadu_si128(reinterpret_cast<const __m128i*>(K256 + 4 * g)));
+            cdgh = _mm_sha256rnds2_epu32(cdgh, abef, wk);            // -> new ABEF; old ABEF is the new CDGH
+            wk = _mm_shuffle_epi32(wk, 0x0E);
+            abef = _mm_sha256rnds2_epu32(abef, cdgh, wk);
+        }
+        abef = _mm_add_epi32(abef, abef0);
+        cdgh = _mm_add_epi32(cdgh, cdgh0);
     }
-    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
+    const __m128i feba = _mm_shuffle_epi32(abef, 0x1B);  // A,B,E,F
+    const __m128i dchg = _mm_shuffle_epi32(cdgh, 0xB1);  // G,H,C,D
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(h), _mm_blend_epi16(feba, dchg, 0xF0));      // A,B,C,D
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(h + 4), _mm_alignr_epi8(dchg, feba, 8));     // E,F,G,H
+}
+
+bool cpu_has_sha() {
+    unsigned a = 0, b = 0, c = 0, d = 0;
+    if (!__get_cpuid_count(7, 0, &a, &b, &c, &d)) return false;
+    return (b >> 29) & 1u;
+}
+#endif
+
+void compress_blocks(uint32_t h[8], const uint8_t* data, size_t nblocks) {
+#if defined(__x86_64__)
+    static const bool ni = cpu_has_sha() && std::getenv("STARK101_NO_SHANI") == nullptr;
+    if (ni) {
+        compress_shani(h, data, nblocks);
+        return;
+    }
+#endif
+    compress_scalar(h, data, nblocks);
 }
 }  // namespace
 
 namespace sha {
-std::array<uint8_t, 32> digest(const uint8_t* data, size_t len) {
+namespace {
+std::array<uint8_t, 32> digest_with(void (*fn)(uint32_t*, const uint8_t*, size_t), const uint8_t* data, size_t len) {
     uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
     size_t full = len / 64;
-    for (size_t i = 0; i < full; i++) compress(h, data + 64 * i);
+    fn(h, data, full);
     uint8_t tail[128] = {0};
     size_t rem = len - 64 * full;
     if (rem) std::memcpy(tail, data + 64 * full, rem);
@@ -58,12 +124,24 @@ std::array<uint8_t, 32> digest(const uint8_t* data, size_t len) {
     size_t tl = rem + 9 <= 64 ? 64 : 128;
     uint64_t bits = static_cast<uint64_t>(len) * 8;
     for (int i = 0; i < 8; i++) tail[tl - 1 - i] = static_cast<uint8_t>(bits >> (8 * i));
-    compress(h, tail);
-    if (tl == 128) compress(h, tail + 64);
+    fn(h, tail, tl / 64);
     std::array<uint8_t, 32> out{};
     for (int i = 0; i < 8; i++)
         for (int j = 0; j < 4; j++) out[4 * i + j] = static_cast<uint8_t>(h[i] >> (24 - 8 * j));
     return out;
+}
+}  // namespace
+
+std::array<uint8_t, 32> digest(const uint8_t* data, size_t len) { return digest_with(compress_blocks, data, len); }
+std::array<uint8_t, 32> digest_portable(const uint8_t* data, size_t len) {
+    return digest_with(compress_scalar, data, len);
+}
+bool accelerated() {
+#if defined(__x86_64__)
+    return cpu_has_sha() && std::getenv("STARK101_NO_SHANI") == nullptr;
+#else
+    return false;
+#endif
 }
 
 std::string hex(const uint8_t* data, size_t len) {

@@ -46,6 +46,11 @@ std::array<uint8_t, 32> digest(const uint8_t* data, size_t len);
 std::string hex(const uint8_t* data, size_t len);            // lowercase
 std::string digest_hex(const std::string& s);                  // sha256::digest(s)
 std::vector<uint8_t> from_hex(const std::string& s);           // throws Panic on bad hex
+// digest() uses the x86 SHA extensions when the CPU has them (runtime check;
+// STARK101_NO_SHANI=1 disables them); digest_portable() is always the plain
+// C++ compression (the tests cross-check the two).
+std::array<uint8_t, 32> digest_portable(const uint8_t* data, size_t len);
+bool accelerated();
 }  // namespace sha
 
 // -------------------------------------------------------------- FieldElement

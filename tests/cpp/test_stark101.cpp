@@ -208,6 +208,15 @@ TEST(cpu, sha256_fips_vectors) {
     std::string a(1000, 'a');
     ASSERT_EQ(sha::digest_hex(a), std::string("41edece42d63e8d9bf515a9ba6932e1c20cbc9f5a5d134645adb5db1b9737ea3"));
 }
+TEST(cpu, sha256_accelerated_matches_portable) {
+    // every tail shape (0..3 blocks + remainder) and a long message
+    std::vector<uint8_t> buf(4096 + 300);
+    for (size_t i = 0; i < buf.size(); i++) buf[i] = static_cast<uint8_t>(i * 131u + (i >> 7));
+    for (size_t len = 0; len <= 300; len++)
+        ASSERT_TRUE(sha::digest(buf.data() + (len & 7), len) == sha::digest_portable(buf.data() + (len & 7), len));
+    ASSERT_TRUE(sha::digest(buf.data(), buf.size()) == sha::digest_portable(buf.data(), buf.size()));
+    std::printf("  (host SHA-256 %s)\n", sha::accelerated() ? "x86 SHA extensions" : "portable");
+}
 TEST(cpu, channel_send_and_draw) {
     FriChannel ch;
     ASSERT_PANICS(ch.receive_random_int(0, 10, false));  // channel.rs:65: "" is not valid hex
