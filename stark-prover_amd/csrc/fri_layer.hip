@@ -160,16 +160,17 @@ __device__ __forceinline__ void quad(const uint4& vals, const uint32_t* in0, uin
     hnode(n0, n1, out);
 }
 
-// Levels l+3, l+4 through LDS: 256 level-(l+2) nodes -> 128 -> 64.
+// Levels l+3, l+4 through LDS: TPB level-(l+2) nodes -> TPB/2 -> TPB/4.
+template <uint32_t TPB>
 __device__ __forceinline__ void lds_two_levels(uint4* lds, const Dg& mine, uint32_t* lv2, uint32_t* lv3, uint32_t* lv4,
                                                size_t g2 /*first level-(l+2) index of this WG*/) {
-    uint4* A = lds;            // 256 digests
-    uint4* B = lds + 512;      // 128 digests
+    uint4* A = lds;             // TPB digests
+    uint4* B = lds + 2 * TPB;   // TPB/2 digests
     const uint32_t t = threadIdx.x;
     dg_store(lv2 + 8 * (g2 + t), mine);
     dg_lds_store(A + 2 * t, mine);
     lds_barrier();
-    if (t < 128) {
+    if (t < TPB / 2) {
         Dg l, r, o;
         dg_lds_load(A + 4 * t, l); dg_lds_load(A + 4 * t + 2, r);
         hnode(l, r, o);
@@ -177,7 +178,7 @@ __device__ __forceinline__ void lds_two_levels(uint4* lds, const Dg& mine, uint3
         dg_store(lv3 + 8 * (g2 / 2 + t), o);
     }
     lds_barrier();
-    if (t < 64) {
+    if (t < TPB / 4) {
         Dg l, r, o;
         dg_lds_load(B + 4 * t, l); dg_lds_load(B + 4 * t + 2, r);
         hnode(l, r, o);
@@ -189,13 +190,14 @@ __device__ __forceinline__ bool gated_off(const LayerTask& t) {
     return t.gst && t.gidx >= 0 && !t.gst->active[t.gidx];
 }
 
-template <bool FOLD, bool COMMIT>
-__global__ __launch_bounds__(256) void k_layer_leaf(LayerTask t) {
+// TPB threads, 4 leaves each: 4*TPB leaves -> TPB/4 level-4 nodes per WG.
+template <bool FOLD, bool COMMIT, uint32_t TPB>
+__global__ __launch_bounds__(TPB) void k_layer_leaf(LayerTask t) {
     if (gated_off(t)) return;
-    __shared__ uint4 lds[512 + 256];
+    __shared__ uint4 lds[3 * TPB];
     __shared__ int32_t red[12];
     const uint32_t L = t.L;
-    const size_t q = (size_t)blockIdx.x * 256 + threadIdx.x;   // quad index: leaves 4q..4q+3
+    const size_t q = (size_t)blockIdx.x * TPB + threadIdx.x;   // quad index: leaves 4q..4q+3
     uint4 v;
     if (FOLD) {
         const size_t half = (size_t)1 << L;
@@ -213,8 +215,8 @@ __global__ __launch_bounds__(256) void k_layer_leaf(LayerTask t) {
     Dg top;
     quad<true>(v, nullptr, tr + 8 * level_offset(L, 0), tr + 8 * level_offset(L, 1), q, top);
     if (COMMIT) coef_task(t, blockIdx.x, gridDim.x, red);
-    lds_two_levels(lds, top, tr + 8 * level_offset(L, 2), tr + 8 * level_offset(L, 3), tr + 8 * level_offset(L, 4),
-                   (size_t)blockIdx.x * 256);
+    lds_two_levels<TPB>(lds, top, tr + 8 * level_offset(L, 2), tr + 8 * level_offset(L, 3),
+                        tr + 8 * level_offset(L, 4), (size_t)blockIdx.x * TPB);
 }
 
 // Wide leaf kernel for narrow layers (2^10 .. 2^18 elements): one leaf per
@@ -603,6 +605,9 @@ static LayerTask with_gate(const LayerTask& in) {
     return t;
 }
 
+#ifndef QUAD_TPB
+#define QUAD_TPB 256         // quad leaf kernel: threads per WG (1024 leaves per WG)
+#endif
 #ifndef QUAD_MIN_LOG
 #define QUAD_MIN_LOG 19      // smaller layers: one leaf per lane (A/B: 19 beats 20 and 21)
 #endif
@@ -626,14 +631,15 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
     }
     uint32_t G, out_per_wg;
     if (L >= QUAD_MIN_LOG) {
-        G = 1u << (L - 10);
-        out_per_wg = 64;
+        constexpr uint32_t TPB = QUAD_TPB;
+        G = (uint32_t)(((size_t)1 << L) / (4 * TPB));
+        out_per_wg = TPB / 4;
         if (fold) {
-            if (commit) hipLaunchKernelGGL((k_layer_leaf<true, true>), dim3(G), dim3(256), 0, s, t);
-            else hipLaunchKernelGGL((k_layer_leaf<true, false>), dim3(G), dim3(256), 0, s, t);
+            if (commit) hipLaunchKernelGGL((k_layer_leaf<true, true, TPB>), dim3(G), dim3(TPB), 0, s, t);
+            else hipLaunchKernelGGL((k_layer_leaf<true, false, TPB>), dim3(G), dim3(TPB), 0, s, t);
         } else {
-            if (commit) hipLaunchKernelGGL((k_layer_leaf<false, true>), dim3(G), dim3(256), 0, s, t);
-            else hipLaunchKernelGGL((k_layer_leaf<false, false>), dim3(G), dim3(256), 0, s, t);
+            if (commit) hipLaunchKernelGGL((k_layer_leaf<false, true, TPB>), dim3(G), dim3(TPB), 0, s, t);
+            else hipLaunchKernelGGL((k_layer_leaf<false, false, TPB>), dim3(G), dim3(TPB), 0, s, t);
         }
     } else {
         G = 1u << (L - 8);
