@@ -362,9 +362,10 @@ __device__ __forceinline__ uint32_t hexhex(uint32_t b) {
 }
 
 // Channel work of one top kernel as a sequence of compression jobs run by
-// wave 7 (lanes redundant), with ONE compress_loop and ONE kwtab_loop call
-// site: the jobs done during the narrow tree levels (off the critical path)
-// leave exactly the code the post-root jobs need in the I-cache.
+// wave 7 (lane pairs redundant), with ONE lane-pair compress and ONE
+// compress_kw call site: the jobs done during the narrow tree levels (off
+// the critical path) leave exactly the code the post-root jobs need in the
+// I-cache.
 //   0  rehash block   X = compress(IV, hex(cs))        channel.rs:75-76, the
 //   1  rehash pad     cs = X = pad(X)                  receive's deferred rehash
 //   2  midstate       X = compress(IV, hex(cs))        first block of the next send
@@ -375,14 +376,17 @@ __device__ __forceinline__ uint32_t hexhex(uint32_t b) {
 //   7  final block 2  cs = X = compress(X, hex(be64(fv)) | pad)   send(final.to_bytes())
 enum { CJ_REHASH = 0, CJ_MID = 2, CJ_ROOT = 3, CJ_FINAL = 6, CJ_END_ROUND = 6, CJ_END_FINAL = 8 };
 
-__device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[8], uint32_t has, const uint4* root_lds,
-                                         uint32_t fv) {
+// Lane-pair form (sha256_quad.hpp): X is this lane's half of the chaining
+// value (even lane words 4..7, odd lane 0..3); cs stays whole on every lane.
+__device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[4], uint32_t has, const uint4* root_lds,
+                                         uint32_t fv, const shaq::Role& R) {
     uint32_t w[16];
     const bool pad = (j == 1) || (j == 5);
     if (j == 0 || j == 2 || j == 6) {
 #pragma unroll
         for (int i = 0; i < 8; i++) hex2(cs[i], w[2 * i], w[2 * i + 1]);
-        sha::init(X);
+#pragma unroll
+        for (int i = 0; i < 4; i++) X[i] = R.iv[i];
     } else if (j == 3 || j == 4) {
         Dg r;
         dg_lds_load(root_lds, r);
@@ -392,7 +396,10 @@ __device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[8], u
             const uint32_t rw = hi ? r.w[4 + (jj >> 2)] : r.w[jj >> 2];
             w[jj] = hexhex((rw >> (24 - 8 * (jj & 3))) & 255u);
         }
-        if (j == 3 && !has) sha::init(X);
+        if (j == 3 && !has) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) X[i] = R.iv[i];
+        }
     } else if (j == 7) {
 #pragma unroll
         for (int i = 0; i < 16; i++) w[i] = 0u;
@@ -401,11 +408,15 @@ __device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[8], u
         w[4] = 0x80000000u;
         w[15] = 80u * 8u;                           // hex(state) (64) + 16 chars
     }
-    if (pad) shaf::kwtab_loop(X, j == 1 ? shaf::PAD_KW_C.kw : (has ? shaf::PAD_KW_1536.kw : shaf::PAD_KW_1024.kw));
-    else shaf::compress_loop(X, w);
-    if (j == 1 || j == 5 || j == 7) {
+    if (pad) shaq::compress_kw(X, j == 1 ? shaf::PAD_KW_C.kw : (has ? shaf::PAD_KW_1536.kw : shaf::PAD_KW_1024.kw), R);
+    else shaq::compress(X, w, R);
+    if (j == 1 || j == 5 || j == 7) {            // cs = X, both halves on every lane
 #pragma unroll
-        for (int i = 0; i < 8; i++) cs[i] = X[i];
+        for (int i = 0; i < 4; i++) {
+            const uint32_t o = shaq::swap01(X[i]);
+            cs[i] = R.is_a ? X[i] : o;
+            cs[4 + i] = R.is_a ? o : X[i];
+        }
     }
 }
 
@@ -440,7 +451,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
 
     const bool chan_wave = COMMIT && tid >= 448;
     DevState* st = t.st;
-    uint32_t cs[8], X[8];
+    uint32_t cs[8], X[4];
     uint32_t has = 0;
     int job = CJ_END_FINAL;
     if (chan_wave) {
@@ -549,7 +560,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         // channel job: during the narrow levels (SIMD 3 idle) only the
         // pre-root jobs, after the last level anything left
         if (chan_wave && job < job_end && (level ? (cnt <= 192 && job < CJ_ROOT) : true)) {
-            chan_job(job, cs, X, has, A, fv);
+            chan_job(job, cs, X, has, A, fv, R);
             job++;
         }
         lds_barrier();
