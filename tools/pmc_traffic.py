@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-DOMINANT_KERNEL = "fri::k_layer_leaf<false, true>"      # layer 0: leaves + levels 1-4
+DOMINANT_KERNEL = "fri::k_layer_leaf<false, true"       # layer 0 (prefix: + ", 256u>"): leaves + levels 1-4
 
 
 def per_launch(path, counter):
@@ -38,12 +38,13 @@ def main():
         wb = 1024.0 * write.get(k, 0.0)
         kernels[k] = {"fetch_bytes_corrected": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
                       "launches_fetch": nf.get(k, 0), "launches_write": nw.get(k, 0)}
-    dom = kernels[DOMINANT_KERNEL]
+    dom_name = next(k for k in kernels if k.startswith(DOMINANT_KERNEL))
+    dom = kernels[dom_name]
     res = {}
     if os.path.exists(out):
         res = json.load(open(out))
     res[str(log_n)] = {
-        "merkle_layer0_leaf": dict(dom, kernel=DOMINANT_KERNEL),
+        "merkle_layer0_leaf": dict(dom, kernel=dom_name),
         "all_kernels_avg_per_launch": kernels,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (csv), KiB -> bytes, "
                   "FETCH_SIZE x2 (gfx950 16-B/lane read correction), averaged over every launch in the run",
