@@ -1,0 +1,81 @@
+// Dev probe: do the tree-top "plateaus" (some levels of a
+// k_tree_top launch take 9-11.4 K cycles per lane-pair node instead of 8.6 K,
+// in ~0.4 K steps, stable once they start) appear outside the FRI kernel?
+// One 512-thread workgroup, 24 levels of 32 lane-pair nodes on wave 0 (each
+// level hashes the previous level's digests), an LDS-only barrier per level
+// for all eight waves, s_memtime around each level's node on lane 0.
+//   mode 0: the other waves only pass the barriers
+//   mode 1: + wave 7 runs one compression in each of the first 3 levels
+//   mode 2: + every level's digests are also stored to HBM (as the tops do)
+//   hipcc -O3 --offload-arch=gfx950 -I../csrc plateau_micro.hip -o plateau_micro
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include "sha256_quad.hpp"
+using namespace fri;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+constexpr int LEVELS = 24;
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* hbm, unsigned long long* clk, int mode) {
+    __shared__ uint4 A[2 * 64], B[2 * 64];
+    const uint32_t tid = threadIdx.x;
+    if (tid < 128) A[tid] = reinterpret_cast<const uint4*>(in)[tid];
+    __syncthreads();
+    const shaq::Role R = shaq::role_of(tid);
+    uint32_t X[4] = {R.iv[0], R.iv[1], R.iv[2], R.iv[3]};
+    uint4* a = A;
+    uint4* b = B;
+    for (int it = 0; it < LEVELS; it++) {
+        if (tid < 64) {                                  // 32 pairs: node q hashes digests q and q+32 (mod 64)
+            const uint32_t q = tid >> 1, half = (tid & 1u) ^ 1u;
+            uint32_t l[8], r[8], o[4];
+            const uint4 l0 = a[2 * q], l1 = a[2 * q + 1], r0 = a[2 * ((q + 16) & 31)], r1 = a[2 * ((q + 16) & 31) + 1];
+            l[0] = l0.x; l[1] = l0.y; l[2] = l0.z; l[3] = l0.w; l[4] = l1.x; l[5] = l1.y; l[6] = l1.z; l[7] = l1.w;
+            r[0] = r0.x; r[1] = r0.y; r[2] = r0.z; r[3] = r0.w; r[4] = r1.x; r[5] = r1.y; r[6] = r1.z; r[7] = r1.w;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+            shaq::node(l, r, o, R);
+            const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+            if (tid == 0) clk[it] = c1 - c0;
+            const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
+            b[2 * q + half] = v;
+            if (mode >= 2) reinterpret_cast<uint4*>(hbm + 8 * (64 * it + q))[half] = v;
+        }
+        if (mode >= 1 && tid >= 448 && it < 3) {         // wave 7: one compression (channel pre-job)
+            uint32_t w[16];
+            for (int i = 0; i < 16; i++) w[i] = it * 16 + i;
+            shaq::compress(X, w, R);
+        }
+        lds_barrier();
+        uint4* t = a; a = b; b = t;
+    }
+    if (tid >= 448 && tid < 452) hbm[8 * 64 * LEVELS + tid - 448] = X[tid & 3];
+}
+
+int main() {
+    uint32_t h_in[512];
+    for (int i = 0; i < 512; i++) h_in[i] = 0x9e3779b9u * (i + 1) ^ (i << 9);
+    uint32_t *d_in, *d_hbm;
+    unsigned long long* d_clk;
+    CK(hipMalloc(&d_in, sizeof(h_in)));
+    CK(hipMalloc(&d_hbm, (8 * 64 * LEVELS + 64) * 4));
+    CK(hipMalloc(&d_clk, LEVELS * 8));
+    CK(hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice));
+    for (int mode = 0; mode < 3; mode++) {
+        printf("mode %d\n", mode);
+        for (int rep = 0; rep < 8; rep++) {
+            hipLaunchKernelGGL(k_plateau, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode);
+            CK(hipDeviceSynchronize());
+            unsigned long long c[LEVELS];
+            CK(hipMemcpy(c, d_clk, sizeof(c), hipMemcpyDeviceToHost));
+            printf("  ");
+            for (int i = 0; i < LEVELS; i++) printf("%.1f ", c[i] / 1000.0);
+            printf("\n");
+        }
+    }
+    return 0;
+}
