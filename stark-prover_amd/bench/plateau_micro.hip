@@ -7,6 +7,10 @@
 //   mode 0: the other waves only pass the barriers
 //   mode 1: + wave 7 runs one compression in each of the first 3 levels
 //   mode 2: + every level's digests are also stored to HBM (as the tops do)
+//   modes 3-5: as mode 2, but the timed region also covers the store and its
+//   completion (s_waitcnt vmcnt(0)); level `it` writes at it * STRIDE[mode]
+//   bytes, so 3 stays in one page and 4/5 touch a new 2 MB / 16 MB region
+//   per level (the tops write each level at its own tree offset)
 //   hipcc -O3 --offload-arch=gfx950 -I../csrc plateau_micro.hip -o plateau_micro
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -20,7 +24,7 @@ constexpr int LEVELS = 24;
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* hbm, unsigned long long* clk, int mode) {
+__global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* hbm, unsigned long long* clk, int mode, size_t stride) {
     __shared__ uint4 A[2 * 64], B[2 * 64];
     const uint32_t tid = threadIdx.x;
     if (tid < 128) A[tid] = reinterpret_cast<const uint4*>(in)[tid];
@@ -39,11 +43,15 @@ __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* h
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             const unsigned long long c0 = __builtin_amdgcn_s_memtime();
             shaq::node(l, r, o, R);
-            const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-            if (tid == 0) clk[it] = c1 - c0;
+            unsigned long long c1 = __builtin_amdgcn_s_memtime();
             const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
             b[2 * q + half] = v;
-            if (mode >= 2) reinterpret_cast<uint4*>(hbm + 8 * (64 * it + q))[half] = v;
+            if (mode >= 2) reinterpret_cast<uint4*>(hbm + it * stride + 8 * q)[half] = v;
+            if (mode >= 3) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                c1 = __builtin_amdgcn_s_memtime();
+            }
+            if (tid == 0) clk[it] = c1 - c0;
         }
         if (mode >= 1 && tid >= 448 && it < 3) {         // wave 7: one compression (channel pre-job)
             uint32_t w[16];
@@ -53,7 +61,7 @@ __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* h
         lds_barrier();
         uint4* t = a; a = b; b = t;
     }
-    if (tid >= 448 && tid < 452) hbm[8 * 64 * LEVELS + tid - 448] = X[tid & 3];
+    if (tid >= 448 && tid < 452) hbm[tid - 448] = X[tid & 3];
 }
 
 int main() {
@@ -62,13 +70,14 @@ int main() {
     uint32_t *d_in, *d_hbm;
     unsigned long long* d_clk;
     CK(hipMalloc(&d_in, sizeof(h_in)));
-    CK(hipMalloc(&d_hbm, (8 * 64 * LEVELS + 64) * 4));
+    const size_t STRIDE[6] = {512, 512, 512, 512, (2u << 20) / 4, (16u << 20) / 4};   // u32 words
+    CK(hipMalloc(&d_hbm, (size_t)LEVELS * STRIDE[5] * 4 + 4096));
     CK(hipMalloc(&d_clk, LEVELS * 8));
     CK(hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice));
-    for (int mode = 0; mode < 3; mode++) {
+    for (int mode = 0; mode < 6; mode++) {
         printf("mode %d\n", mode);
         for (int rep = 0; rep < 8; rep++) {
-            hipLaunchKernelGGL(k_plateau, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode);
+            hipLaunchKernelGGL(k_plateau, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode, STRIDE[mode]);
             CK(hipDeviceSynchronize());
             unsigned long long c[LEVELS];
             CK(hipMemcpy(c, d_clk, sizeof(c), hipMemcpyDeviceToHost));
