@@ -11,6 +11,10 @@
 //   completion (s_waitcnt vmcnt(0)); level `it` writes at it * STRIDE[mode]
 //   bytes, so 3 stays in one page and 4/5 touch a new 2 MB / 16 MB region
 //   per level (the tops write each level at its own tree offset)
+//   mode 6: as mode 0, but wave 7 runs ~10 KB of distinct straight-line code
+//   per level, cycling through 6 variants (~60 KB: instruction-cache
+//   pressure from a concurrent wave, as the channel wave of k_tree_top adds)
+//   mode 7: as mode 6 with one variant every level (warm after level 0)
 //   hipcc -O3 --offload-arch=gfx950 -I../csrc plateau_micro.hip -o plateau_micro
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -23,6 +27,27 @@ using namespace fri;
 constexpr int LEVELS = 24;
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int V>
+__device__ __attribute__((noinline)) uint32_t junk(uint32_t a, uint32_t b) {
+#pragma unroll
+    for (int i = 0; i < 256; i++) {
+        a = __builtin_rotateleft32(a ^ (b + 0x9e3779b9u * (uint32_t)(i + 97 * V)), (i + V) % 31 + 1);
+        b += a ^ (uint32_t)(7919 * V + 131 * i);
+    }
+    return a ^ b;
+}
+
+__device__ uint32_t junk_any(int v, uint32_t a, uint32_t b) {
+    switch (v) {
+        case 0: return junk<0>(a, b);
+        case 1: return junk<1>(a, b);
+        case 2: return junk<2>(a, b);
+        case 3: return junk<3>(a, b);
+        case 4: return junk<4>(a, b);
+        default: return junk<5>(a, b);
+    }
+}
 
 __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* hbm, unsigned long long* clk, int mode, size_t stride) {
     __shared__ uint4 A[2 * 64], B[2 * 64];
@@ -46,14 +71,15 @@ __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* h
             unsigned long long c1 = __builtin_amdgcn_s_memtime();
             const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
             b[2 * q + half] = v;
-            if (mode >= 2) reinterpret_cast<uint4*>(hbm + it * stride + 8 * q)[half] = v;
-            if (mode >= 3) {
+            if (mode >= 2 && mode < 6) reinterpret_cast<uint4*>(hbm + it * stride + 8 * q)[half] = v;
+            if (mode >= 3 && mode < 6) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 c1 = __builtin_amdgcn_s_memtime();
             }
             if (tid == 0) clk[it] = c1 - c0;
         }
-        if (mode >= 1 && tid >= 448 && it < 3) {         // wave 7: one compression (channel pre-job)
+        if (mode >= 6 && tid >= 448) X[0] ^= junk_any(mode == 6 ? it % 6 : 0, X[1] + it, tid);
+        if (mode >= 1 && mode < 6 && tid >= 448 && it < 3) {         // wave 7: one compression (channel pre-job)
             uint32_t w[16];
             for (int i = 0; i < 16; i++) w[i] = it * 16 + i;
             shaq::compress(X, w, R);
@@ -70,11 +96,11 @@ int main() {
     uint32_t *d_in, *d_hbm;
     unsigned long long* d_clk;
     CK(hipMalloc(&d_in, sizeof(h_in)));
-    const size_t STRIDE[6] = {512, 512, 512, 512, (2u << 20) / 4, (16u << 20) / 4};   // u32 words
+    const size_t STRIDE[8] = {512, 512, 512, 512, (2u << 20) / 4, (16u << 20) / 4, 512, 512};   // u32 words
     CK(hipMalloc(&d_hbm, (size_t)LEVELS * STRIDE[5] * 4 + 4096));
     CK(hipMalloc(&d_clk, LEVELS * 8));
     CK(hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice));
-    for (int mode = 0; mode < 6; mode++) {
+    for (int mode = 0; mode < 8; mode++) {
         printf("mode %d\n", mode);
         for (int rep = 0; rep < 8; rep++) {
             hipLaunchKernelGGL(k_plateau, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode, STRIDE[mode]);
