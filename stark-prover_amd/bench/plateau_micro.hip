@@ -15,6 +15,8 @@
 //   per level, cycling through 6 variants (~60 KB: instruction-cache
 //   pressure from a concurrent wave, as the channel wave of k_tree_top adds)
 //   mode 7: as mode 6 with one variant every level (warm after level 0)
+//   mode 8: as mode 0 with k_tree_top's LDS layout and addressing: 48 KB
+//   array, B 32 KB above A, node q reads digests 2q and 2q+1 (pair_level)
 //   hipcc -O3 --offload-arch=gfx950 -I../csrc plateau_micro.hip -o plateau_micro
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -49,8 +51,11 @@ __device__ uint32_t junk_any(int v, uint32_t a, uint32_t b) {
     }
 }
 
+template <bool TOP_LDS>
 __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* hbm, unsigned long long* clk, int mode, size_t stride) {
-    __shared__ uint4 A[2 * 64], B[2 * 64];
+    __shared__ uint4 lds[TOP_LDS ? 3 * 1024 : 4 * 64];
+    uint4* A = lds;
+    uint4* B = lds + (TOP_LDS ? 2 * 1024 : 2 * 64);
     const uint32_t tid = threadIdx.x;
     if (tid < 128) A[tid] = reinterpret_cast<const uint4*>(in)[tid];
     __syncthreads();
@@ -62,7 +67,8 @@ __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* h
         if (tid < 64) {                                  // 32 pairs: node q hashes digests q and q+32 (mod 64)
             const uint32_t q = tid >> 1, half = (tid & 1u) ^ 1u;
             uint32_t l[8], r[8], o[4];
-            const uint4 l0 = a[2 * q], l1 = a[2 * q + 1], r0 = a[2 * ((q + 16) & 31)], r1 = a[2 * ((q + 16) & 31) + 1];
+            const uint32_t li = TOP_LDS ? 4 * q : 2 * q, ri = TOP_LDS ? 4 * q + 2 : 2 * ((q + 16) & 31);
+            const uint4 l0 = a[li], l1 = a[li + 1], r0 = a[ri], r1 = a[ri + 1];
             l[0] = l0.x; l[1] = l0.y; l[2] = l0.z; l[3] = l0.w; l[4] = l1.x; l[5] = l1.y; l[6] = l1.z; l[7] = l1.w;
             r[0] = r0.x; r[1] = r0.y; r[2] = r0.z; r[3] = r0.w; r[4] = r1.x; r[5] = r1.y; r[6] = r1.z; r[7] = r1.w;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -96,14 +102,15 @@ int main() {
     uint32_t *d_in, *d_hbm;
     unsigned long long* d_clk;
     CK(hipMalloc(&d_in, sizeof(h_in)));
-    const size_t STRIDE[8] = {512, 512, 512, 512, (2u << 20) / 4, (16u << 20) / 4, 512, 512};   // u32 words
+    const size_t STRIDE[9] = {512, 512, 512, 512, (2u << 20) / 4, (16u << 20) / 4, 512, 512, 512};   // u32 words
     CK(hipMalloc(&d_hbm, (size_t)LEVELS * STRIDE[5] * 4 + 4096));
     CK(hipMalloc(&d_clk, LEVELS * 8));
     CK(hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice));
-    for (int mode = 0; mode < 8; mode++) {
+    for (int mode = 0; mode < 9; mode++) {
         printf("mode %d\n", mode);
         for (int rep = 0; rep < 8; rep++) {
-            hipLaunchKernelGGL(k_plateau, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode, STRIDE[mode]);
+            if (mode == 8) hipLaunchKernelGGL(k_plateau<true>, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, 0, STRIDE[mode]);
+            else hipLaunchKernelGGL(k_plateau<false>, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode, STRIDE[mode]);
             CK(hipDeviceSynchronize());
             unsigned long long c[LEVELS];
             CK(hipMemcpy(c, d_clk, sizeof(c), hipMemcpyDeviceToHost));
