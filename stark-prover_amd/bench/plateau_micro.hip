@@ -51,7 +51,7 @@ __device__ uint32_t junk_any(int v, uint32_t a, uint32_t b) {
     }
 }
 
-template <bool TOP_LDS>
+template <bool TOP_LDS, bool PRESSURE = false>
 __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* hbm, unsigned long long* clk, int mode, size_t stride) {
     __shared__ uint4 lds[TOP_LDS ? 3 * 1024 : 4 * 64];
     uint4* A = lds;
@@ -63,8 +63,13 @@ __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* h
     uint32_t X[4] = {R.iv[0], R.iv[1], R.iv[2], R.iv[3]};
     uint4* a = A;
     uint4* b = B;
+    constexpr int NP = PRESSURE ? 48 : 1;
+    uint32_t pad[NP];
+#pragma unroll
+    for (int i = 0; i < NP; i++) pad[i] = in[(tid + 7 * i) & 511];
     for (int it = 0; it < LEVELS; it++) {
-        if (tid < 64) {                                  // 32 pairs: node q hashes digests q and q+32 (mod 64)
+        const uint32_t active = mode == 10 ? 64u >> (it % 6) : 64u;
+        if (tid < active) {                              // 32 pairs: node q hashes digests q and q+32 (mod 64)
             const uint32_t q = tid >> 1, half = (tid & 1u) ^ 1u;
             uint32_t l[8], r[8], o[4];
             const uint32_t li = TOP_LDS ? 4 * q : 2 * q, ri = TOP_LDS ? 4 * q + 2 : 2 * ((q + 16) & 31);
@@ -84,16 +89,26 @@ __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* h
             }
             if (tid == 0) clk[it] = c1 - c0;
         }
-        if (mode >= 6 && tid >= 448) X[0] ^= junk_any(mode == 6 ? it % 6 : 0, X[1] + it, tid);
+        if (mode >= 6 && mode < 8 && tid >= 448) X[0] ^= junk_any(mode == 6 ? it % 6 : 0, X[1] + it, tid);
         if (mode >= 1 && mode < 6 && tid >= 448 && it < 3) {         // wave 7: one compression (channel pre-job)
             uint32_t w[16];
             for (int i = 0; i < 16; i++) w[i] = it * 16 + i;
             shaq::compress(X, w, R);
         }
+        if (PRESSURE) {
+#pragma unroll
+            for (int i = 0; i < NP; i++) asm volatile("" : "+v"(pad[i]));
+        }
         lds_barrier();
         uint4* t = a; a = b; b = t;
     }
     if (tid >= 448 && tid < 452) hbm[tid - 448] = X[tid & 3];
+    if (PRESSURE) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < NP; i++) acc += pad[i] * (i + 1);
+        hbm[64 + tid] = acc;
+    }
 }
 
 int main() {
@@ -102,14 +117,15 @@ int main() {
     uint32_t *d_in, *d_hbm;
     unsigned long long* d_clk;
     CK(hipMalloc(&d_in, sizeof(h_in)));
-    const size_t STRIDE[9] = {512, 512, 512, 512, (2u << 20) / 4, (16u << 20) / 4, 512, 512, 512};   // u32 words
+    const size_t STRIDE[11] = {512, 512, 512, 512, (2u << 20) / 4, (16u << 20) / 4, 512, 512, 512, 512, 512};   // u32 words
     CK(hipMalloc(&d_hbm, (size_t)LEVELS * STRIDE[5] * 4 + 4096));
     CK(hipMalloc(&d_clk, LEVELS * 8));
     CK(hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice));
-    for (int mode = 0; mode < 9; mode++) {
+    for (int mode = 0; mode < 11; mode++) {
         printf("mode %d\n", mode);
         for (int rep = 0; rep < 8; rep++) {
-            if (mode == 8) hipLaunchKernelGGL(k_plateau<true>, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, 0, STRIDE[mode]);
+            if (mode == 9) hipLaunchKernelGGL((k_plateau<true, true>), dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, 0, STRIDE[mode]);
+            else if (mode >= 8) hipLaunchKernelGGL(k_plateau<true>, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode == 10 ? 10 : 0, STRIDE[mode]);
             else hipLaunchKernelGGL(k_plateau<false>, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode, STRIDE[mode]);
             CK(hipDeviceSynchronize());
             unsigned long long c[LEVELS];

@@ -82,13 +82,20 @@ __device__ __forceinline__ void cleaf(uint32_t v, Dg& o) { shaf::leaf_compact(v,
 // digest words 4..7, the odd lane words 0..3 (LDS for the next level, HBM).
 __device__ __forceinline__ void pair_level(const uint4* A, uint4* B, uint32_t* out, uint32_t tid, uint32_t cnt,
                                            const shaq::Role& R) {
-    if (tid >= 2 * cnt) return;
-    const uint32_t q = tid >> 1, half = (tid & 1u) ^ 1u;
+    // Below 32 nodes the whole of wave 0 still runs: the spare lane pairs
+    // recompute node (q mod cnt) and store nothing. A partly masked wave runs
+    // the node 0.7-2.7 K cycles slower than a full one (8.4 K), by an amount
+    // that changes from launch to launch (bench/plateau_micro.hip mode 10,
+    // profiles/r01_plateau_micro_masked.txt). cnt is a power of two.
+    if (tid >= max(2 * cnt, 64u)) return;
+    const uint32_t q = (tid >> 1) & (cnt - 1), half = (tid & 1u) ^ 1u;
+    const bool real = tid < 2 * cnt;
     Dg a, b;
     dg_lds_load(A + 4 * q, a);
     dg_lds_load(A + 4 * q + 2, b);
     uint32_t o[4];
     shaq::node(a.w, b.w, o, R);
+    if (!real) return;
     const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
     B[2 * q + half] = v;
     reinterpret_cast<uint4*>(out + 8 * q)[half] = v;
