@@ -103,6 +103,10 @@ __global__ __launch_bounds__(512) void k_plateau(const uint32_t* in, uint32_t* h
         uint4* t = a; a = b; b = t;
     }
     if (tid >= 448 && tid < 452) hbm[tid - 448] = X[tid & 3];
+    if (tid == 0) {                                      // placement of this launch: XCC_ID, HW_ID
+        clk[LEVELS] = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+        clk[LEVELS + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
     if (PRESSURE) {
         uint32_t acc = 0;
 #pragma unroll
@@ -119,7 +123,7 @@ int main() {
     CK(hipMalloc(&d_in, sizeof(h_in)));
     const size_t STRIDE[11] = {512, 512, 512, 512, (2u << 20) / 4, (16u << 20) / 4, 512, 512, 512, 512, 512};   // u32 words
     CK(hipMalloc(&d_hbm, (size_t)LEVELS * STRIDE[5] * 4 + 4096));
-    CK(hipMalloc(&d_clk, LEVELS * 8));
+    CK(hipMalloc(&d_clk, (LEVELS + 2) * 8));
     CK(hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice));
     for (int mode = 0; mode < 11; mode++) {
         printf("mode %d\n", mode);
@@ -128,11 +132,11 @@ int main() {
             else if (mode >= 8) hipLaunchKernelGGL(k_plateau<true>, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode == 10 ? 10 : 0, STRIDE[mode]);
             else hipLaunchKernelGGL(k_plateau<false>, dim3(1), dim3(512), 0, 0, d_in, d_hbm, d_clk, mode, STRIDE[mode]);
             CK(hipDeviceSynchronize());
-            unsigned long long c[LEVELS];
+            unsigned long long c[LEVELS + 2];
             CK(hipMemcpy(c, d_clk, sizeof(c), hipMemcpyDeviceToHost));
             printf("  ");
             for (int i = 0; i < LEVELS; i++) printf("%.1f ", c[i] / 1000.0);
-            printf("\n");
+            printf(" xcc=%llu hw_id=0x%08llx\n", c[LEVELS], c[LEVELS + 1]);
         }
     }
     return 0;
