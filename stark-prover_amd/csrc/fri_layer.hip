@@ -477,18 +477,24 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     if (FROM_LEAVES) {
         const size_t half = (size_t)1 << L;
         const uint32_t beta_m = FOLD ? (COMMIT ? st->beta_mont[t.k - 1] : t.beta_m) : 0u;
-        for (uint32_t i = tid; i < N; i += blockDim.x) {
+        // under 64 leaves the spare lanes of wave 0 hash leaf (i mod N) and
+        // store nothing: a partly masked wave is slower (see pair_level)
+        for (uint32_t i = tid; i < max(N, 64u); i += blockDim.x) {
+            const uint32_t j = i & (N - 1);          // N is a power of two
+            const bool real = i < N;
             uint32_t v;
             if (FOLD) {
-                v = fold1(t.prev[i], t.prev[i + half], t.xinv[i], beta_m);
-                t.values[i] = v;
+                v = fold1(t.prev[j], t.prev[j + half], t.xinv[j], beta_m);
+                if (real) t.values[j] = v;
             } else {
-                v = t.values[i];
+                v = t.values[j];
             }
             Dg d;
             cleaf(v, d);
-            dg_store(tr + 8 * i, d);
-            dg_lds_store(A + 2 * i, d);
+            if (real) {
+                dg_store(tr + 8 * j, d);
+                dg_lds_store(A + 2 * j, d);
+            }
         }
         if (COMMIT) coef_task(t, 0, 1, red);       // per-wave maxima in red[], wgmax[0..2]
     } else {
