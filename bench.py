@@ -241,24 +241,34 @@ def main():
         if launches:
             avg_ms = ms / launches
             per_launch = nbytes / launches
-            achieved = per_launch / (avg_ms * 1e-3) / 1e9
-            roofline = {"bound": "hbm", "kernel": "k_layer_leaf (layer 0: leaves + tree levels 1-4)",
-                        "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                        "bytes_per_launch": per_launch, "avg_launch_ms": round(avg_ms, 4),
-                        "launches": launches}
-            # The honest bound for SHA-256 Merkle work is int32 VALU issue
-            # (DESIGN.md "VALU cost model"): leaf hash 2009 issue units, node
-            # hash 3592 (v_alignbit/v_add3 are half rate on gfx950).  The leaf
-            # kernel hashes 2^L leaves and (15/16) 2^L nodes (levels 1..4).
+            hbm_gbs = per_launch / (avg_ms * 1e-3) / 1e9
+            # SHA-256 Merkle work is bound by int32 VALU issue:
+            # leaf hash 2009 issue units, node hash 3592 (v_alignbit/v_add3
+            # are half rate on gfx950).  The leaf kernel hashes 2^L leaves and
+            # (15/16) 2^L nodes (levels 1..4).
             nleaf = 1 << blk_log
             units = nleaf * 2009.0 + (15.0 / 16.0) * nleaf * 3592.0
-            roofline["valu"] = {"issue_units_per_launch": units,
-                                "achieved_T_units_s": round(units / (avg_ms * 1e-3) / 1e12, 2),
-                                "peak_T_units_s": VALU_PEAK_TOPS,
-                                "frac": round(units / (avg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
-                                "measured_ceiling_T_units_s": VALU_MEASURED_TOPS,
-                                "frac_of_measured_ceiling": round(units / (avg_ms * 1e-3) / 1e12 / VALU_MEASURED_TOPS, 4)}
+            valu_t = units / (avg_ms * 1e-3) / 1e12
+            hbm = {"achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": per_launch}
+            valu = {"achieved": round(valu_t, 2), "peak": VALU_PEAK_TOPS, "unit": "T int32 lane-ops/s",
+                    "frac": round(valu_t / VALU_PEAK_TOPS, 4), "issue_units_per_launch": units,
+                    "measured_ceiling": VALU_MEASURED_TOPS,
+                    "frac_of_measured_ceiling": round(valu_t / VALU_MEASURED_TOPS, 4)}
+            # the bound is whichever resource the kernel uses the larger share of
+            bound, top = ("valu", valu) if valu["frac"] >= hbm["frac"] else ("hbm", hbm)
+            roofline = {"bound": bound, "kernel": "k_layer_leaf (layer 0: leaves + tree levels 1-4)",
+                        "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"], "frac": top["frac"],
+                        "traffic": None, "avg_launch_ms": round(avg_ms, 4), "launches": launches,
+                        "hbm": hbm, "valu": valu}
+            # the HBM-bound kernel of the path: the coset-LDE NTT (algorithmic
+            # bytes 4d read + 4n written per commit)
+            lms, ll, lbytes = ctx.profile("lde")
+            if ll:
+                lde_gbs = (lbytes / ll) / (lms / ll * 1e-3) / 1e9
+                roofline["lde_ntt"] = {"bound": "hbm", "achieved": round(lde_gbs, 2), "peak": HBM_PEAK_GBS,
+                                       "unit": "GB/s", "frac": round(lde_gbs / HBM_PEAK_GBS, 4),
+                                       "bytes_per_launch": lbytes / ll, "avg_launch_ms": round(lms / ll, 4)}
         breakdown = {}
         for cls in ("lde", "alltoall", "merkle_layer0_leaf", "layer0", "layers", "gather"):
             cms, cl, _ = ctx.profile(cls)

@@ -190,6 +190,14 @@ int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t
  * reads without a copy.  Valid until fri_ctx_destroy. */
 int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
 
+/* Which commit the read-backs below serve: `generation` grows with every
+ * commit call on the context (successful or not), log_n / n_layers describe
+ * the resident commit (n_layers = 0 when the last commit failed).  A binding
+ * that hands out FRIProof objects records the generation at commit time and
+ * refuses read-backs once it has moved on (the reference's FRIProof owns its
+ * layers, src/fri/fri_commit.rs:9-13; here they live in the context). */
+int fri_commit_info(fri_ctx* ctx, uint64_t* generation, uint32_t* log_n, uint32_t* n_layers);
+
 /* Read-back of the last commit (FRIProof::fri_layers / fri_merkles). */
 int fri_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out, size_t cap);
 /* Merkle level `level` (0 = leaf hashes) of layer `layer`, as 32-byte digests. */

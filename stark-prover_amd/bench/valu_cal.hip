@@ -69,6 +69,66 @@ __global__ __launch_bounds__(256) void k_mad64(unsigned* out, int iters) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+// Sigma-style rotations: 3 alignbit + xor3 vs (x,x) pair + 3 64-bit shifts + xor3
+__global__ __launch_bounds__(256) void k_sig_align(unsigned* out, int iters) {
+    unsigned r[8];
+    for (int i = 0; i < 8; i++) r[i] = threadIdx.x * 7 + i;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            unsigned a, b, c, x = r[i];
+            asm volatile("v_alignbit_b32 %0, %1, %1, 6" : "=v"(a) : "v"(x));
+            asm volatile("v_alignbit_b32 %0, %1, %1, 11" : "=v"(b) : "v"(x));
+            asm volatile("v_alignbit_b32 %0, %1, %1, 25" : "=v"(c) : "v"(x));
+            asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r[i]) : "v"(a), "v"(b), "v"(c));
+        }
+    }
+    unsigned x = 0;
+    for (int i = 0; i < 8; i++) x ^= r[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+__global__ __launch_bounds__(256) void k_sig_64(unsigned* out, int iters) {
+    unsigned r[8];
+    for (int i = 0; i < 8; i++) r[i] = threadIdx.x * 7 + i;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            unsigned long long p, a, b, c;
+            asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[0,0]" : "=v"(p) : "v"((unsigned long long)r[i]));
+            asm volatile("v_lshrrev_b64 %0, 6, %1" : "=v"(a) : "v"(p));
+            asm volatile("v_lshrrev_b64 %0, 11, %1" : "=v"(b) : "v"(p));
+            asm volatile("v_lshrrev_b64 %0, 25, %1" : "=v"(c) : "v"(p));
+            asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r[i]) : "v"((unsigned)a), "v"((unsigned)b), "v"((unsigned)c));
+        }
+    }
+    unsigned x = 0;
+    for (int i = 0; i < 8; i++) x ^= r[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+__global__ __launch_bounds__(256) void k_pkmov(unsigned* out, int iters) {
+    unsigned long long r[8];
+    for (int i = 0; i < 8; i++) r[i] = (unsigned long long)(threadIdx.x * 7 + i) * 0x100000001ull;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[1,0]" : "=v"(r[i]) : "v"(r[(i + 1) & 7]));
+    }
+    unsigned x = 0;
+    for (int i = 0; i < 8; i++) x ^= (unsigned)r[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+__global__ __launch_bounds__(256) void k_lshladd64(unsigned* out, int iters) {
+    unsigned long long r[8];
+    for (int i = 0; i < 8; i++) r[i] = (unsigned long long)(threadIdx.x * 7 + i) * 0x100000001ull;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("v_lshl_add_u64 %0, %1, 3, %2" : "=v"(r[i]) : "v"(r[(i + 1) & 7]), "v"(r[(i + 3) & 7]));
+    }
+    unsigned x = 0;
+    for (int i = 0; i < 8; i++) x ^= (unsigned)r[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+KERNEL(k_pklshr16, BODYSH, "v_pk_lshrrev_b16")
+
 int main() {
     unsigned* o;
     CK(hipMalloc(&o, 4096 * 256 * 4));
@@ -81,7 +141,7 @@ int main() {
               {"v_bfi_b32", k_bfi, 16}, {"v_or3_b32", k_or3, 16}, {"v_and_or_b32", k_and_or, 16},
               {"v_perm_b32", k_perm, 16}, {"v_mul_lo_u32", k_mul_lo, 16}, {"v_mul_hi_u32", k_mul_hi, 16},
               {"v_mad_u32_u24", k_mad24, 16}, {"v_mov_b32", k_mov, 16}, {"v_not_b32", k_not, 16},
-              {"v_lshrrev_b64", k_lshr64, 8}, {"v_mad_u64_u32", k_mad64, 8}};
+              {"v_lshrrev_b64", k_lshr64, 8}, {"v_mad_u64_u32", k_mad64, 8}, {"Sigma align x3+xor3 (4 ins)", k_sig_align, 8}, {"Sigma pkmov+lshr64x3+xor3 (5 ins)", k_sig_64, 8}, {"v_pk_mov_b32", k_pkmov, 8}, {"v_lshl_add_u64", k_lshladd64, 8}, {"v_pk_lshrrev_b16", k_pklshr16, 16}};
     const int iters = 2048;
     for (auto& k : ks) {
         hipLaunchKernelGGL(k.f, dim3(4096), dim3(256), 0, 0, o, iters);

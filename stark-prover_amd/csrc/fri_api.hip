@@ -100,6 +100,8 @@ struct fri_ctx {
     hipStream_t cstream = nullptr;  // coefficient-fold stream (overlaps the local tree)
     hipEvent_t ev_pre = nullptr, ev_coef = nullptr;
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
+    uint64_t commit_gen = 0;        // bumped by every commit: read-backs of an older proof are refused
+    uint32_t commit_log_n = 0;      // codeword log2 of the resident commit
     uint32_t* dq_buf = nullptr;     // decommitment gather staging (64 KiB)
     uint32_t* dq_host = nullptr;    // ... and its pinned host mirror (one DMA per query)
     uint32_t* trace_tree = nullptr; // Merkle tree of the last fri_trace_commit LDE
@@ -598,7 +600,8 @@ static void enqueue_commit(fri_ctx* ctx) {
 static void init_state(fri_ctx* ctx, const fri_channel_state* chan_in, uint32_t flags,
                        const uint32_t* forced_betas) {
     DevState* h = ctx->h_state;
-    memset(h, 0, sizeof(DevState));
+    memset(h, 0, sizeof(DevState));      // n_layers = 0: nothing readable until this commit succeeds
+    ctx->commit_gen++;
     if (chan_in && chan_in->has_state) {
         for (int i = 0; i < 8; i++)
             h->chan[i] = ((uint32_t)chan_in->digest[4 * i] << 24) | ((uint32_t)chan_in->digest[4 * i + 1] << 16) |
@@ -657,8 +660,12 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
     FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
     FRI_HIP(ctx, hipStreamSynchronize(s));
     if (ctx->profiling) spans_collect(ctx);
-    const DevState* h = ctx->h_state;
-    if (h->status) return fail(ctx, (int)h->status, "degree exceeds the domain (reference would panic)");
+    DevState* h = ctx->h_state;
+    if (h->status) {
+        h->n_layers = 0;                 // the failed commit's layers are not served by the read-backs
+        return fail(ctx, (int)h->status, "degree exceeds the domain (reference would panic)");
+    }
+    ctx->commit_log_n = log_n;
     memset(out, 0, sizeof *out);
     out->n_layers = h->n_layers;
     out->n_rounds = h->n_rounds;
@@ -694,6 +701,14 @@ extern "C" int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr) {
     // skips the copy when the pointers match.
     if (!ctx->plan.valid || ctx->plan.d != d) return fail(ctx, FRI_ESTATE, "build a plan first (commit once with this d)");
     *d_ptr = ctx->plan.d_in;
+    return FRI_OK;
+}
+
+extern "C" int fri_commit_info(fri_ctx* ctx, uint64_t* generation, uint32_t* log_n, uint32_t* n_layers) {
+    if (!ctx || !generation || !log_n || !n_layers) return fail(ctx, FRI_EINVAL, "null argument");
+    *generation = ctx->commit_gen;
+    *n_layers = ctx->h_state->n_layers;
+    *log_n = *n_layers ? ctx->commit_log_n : 0u;
     return FRI_OK;
 }
 
@@ -844,8 +859,10 @@ extern "C" int fri_fibsq_composition_commit(fri_ctx* ctx, uint32_t log_t, uint32
     FRI_HIP(ctx, hipGetLastError());
     int rc = run_commit(ctx, nullptr, ctx->scratch_b, n, L, offset, chan_in, flags, nullptr, out);
     if (rc) return rc;
-    if (ctx->h_state->deg[0] > (int32_t)T)
+    if (ctx->h_state->deg[0] > (int32_t)T) {
+        ctx->h_state->n_layers = 0;      // no proof of a violated trace is served
         return fail(ctx, FRI_EDEGREE, "composition polynomial degree exceeds T: the trace violates the constraints");
+    }
     return FRI_OK;
 }
 
@@ -1170,6 +1187,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     if (offset == 0 || offset >= P) return fail(ctx, FRI_EINVAL, "offset must be a nonzero canonical element");
     if ((flags & FRI_FLAG_FORCE_BETAS) && !forced_betas) return fail(ctx, FRI_EINVAL, "forced betas missing");
     if (host_coeffs && !check_canonical(host_coeffs, d)) return fail(ctx, FRI_EINVAL, "coefficient not canonical");
+    if (forced_betas && (flags & FRI_FLAG_FORCE_BETAS) && !check_canonical(forced_betas, MAXR))
+        return fail(ctx, FRI_EINVAL, "forced beta not canonical");
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     int rc = plan_build(ctx, d, log_n, offset);
     if (rc) return rc;
@@ -1341,8 +1360,12 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
     FRI_HIP(ctx, hipStreamSynchronize(s));
     if (ctx->profiling) spans_collect(ctx);
-    const DevState* h = ctx->h_state;
-    if (h->status) return fail(ctx, (int)h->status, "degree exceeds the domain (reference would panic)");
+    DevState* h = ctx->h_state;
+    if (h->status) {
+        h->n_layers = 0;                 // the failed commit's layers are not served by the read-backs
+        return fail(ctx, (int)h->status, "degree exceeds the domain (reference would panic)");
+    }
+    ctx->commit_log_n = log_n;
     memset(out, 0, sizeof *out);
     out->n_layers = h->n_layers;
     out->n_rounds = h->n_rounds;

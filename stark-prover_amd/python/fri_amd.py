@@ -98,6 +98,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_commit_device": (i32, [vp, vp, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
                                     ctypes.POINTER(CommitResult)]),
         "fri_ctx_input_buffer": (i32, [vp, sz, ctypes.POINTER(vp)]),
+        "fri_commit_info": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "fri_layer_copy": (i32, [vp, u32, pu32, sz]),
         "fri_tree_level_copy": (i32, [vp, u32, u32, ctypes.c_char_p, sz]),
         "fri_auth_path": (i32, [vp, u32, ctypes.c_uint64, pu32, ctypes.c_char_p, ctypes.POINTER(u32)]),
@@ -231,12 +232,30 @@ class Context:
                                         _ptr(fb) if fb is not None else None, ctypes.byref(res)))
         return res
 
-    def layer(self, k: int, log_n: int) -> np.ndarray:
+    def commit_info(self):
+        """(generation, log_n, n_layers) of the resident commit (fri_commit_info)."""
+        g, ln, nl = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.lib.fri_commit_info(self.h, ctypes.byref(g), ctypes.byref(ln), ctypes.byref(nl)))
+        return g.value, ln.value, nl.value
+
+    def _resident(self, log_n: int, generation: Optional[int] = None) -> None:
+        """Read-backs serve only the commit they were asked for: the resident
+        codeword must be 2^log_n and, for a FRIProof, still the commit of
+        ``generation`` (a later commit on this context replaced its layers)."""
+        g, ln, nl = self.commit_info()
+        if generation is not None and g != generation:
+            raise FriError(FRI_ESTATE, "FRIProof layers were replaced by a later commit on the same context")
+        if nl and ln != log_n:
+            raise FriError(FRI_ESTATE, f"resident commit is 2^{ln}, not 2^{log_n}")
+
+    def layer(self, k: int, log_n: int, generation: Optional[int] = None) -> np.ndarray:
+        self._resident(log_n, generation)
         out = np.empty(1 << (log_n - k), dtype=np.uint32)
         self._check(self.lib.fri_layer_copy(self.h, k, _ptr(out), out.size))
         return out
 
     def tree_level(self, k: int, level: int, log_n: int) -> List[bytes]:
+        self._resident(log_n)
         cnt = 1 << (log_n - k - level)
         buf = ctypes.create_string_buffer(32 * cnt)
         self._check(self.lib.fri_tree_level_copy(self.h, k, level, buf, 32 * cnt))
@@ -244,6 +263,7 @@ class Context:
         return [raw[32 * i: 32 * i + 32] for i in range(cnt)]
 
     def auth_path(self, k: int, index: int, log_n: int):
+        self._resident(log_n)
         depth = log_n - k
         buf = ctypes.create_string_buffer(32 * max(depth, 1))
         val = ctypes.c_uint32()
@@ -298,9 +318,12 @@ class Context:
         pl = 32 * depth
         return [(int(vals[j]), buf.raw[j * pl:(j + 1) * pl]) for j in range(count)]
 
-    def decommit_query(self, index: int, n_layers: int, log_n: int):
+    def decommit_query(self, index: int, n_layers: int, log_n: int, generation: Optional[int] = None):
         """fri_decommit_query: per committed layer k, (value[idx], value[sib],
         path(idx), path(sib)) with idx = index % m_k, sib = (idx + m_k/2) % m_k."""
+        self._resident(log_n, generation)
+        if n_layers != self.commit_info()[2]:
+            raise FriError(FRI_ESTATE, "layer count differs from the resident commit")
         vals = np.empty(2 * n_layers, dtype=np.uint32)
         total = sum(64 * (log_n - k) for k in range(n_layers))
         buf = ctypes.create_string_buffer(max(total, 1))
@@ -469,13 +492,14 @@ class FRIProof:
     betas: List[int]
     final_value: int
     final_degree: int
+    generation: int = 0      # fri_commit_info generation of the commit that made it
 
     @property
     def n_layers(self) -> int:
         return len(self.roots)
 
     def layer(self, k: int) -> np.ndarray:
-        return self.ctx.layer(k, self.log_n)
+        return self.ctx.layer(k, self.log_n, self.generation)
 
     @property
     def fri_layers(self) -> List[np.ndarray]:
@@ -493,7 +517,7 @@ def decommit_fri_layers(index: int, proof: "FRIProof", channel: Channel) -> None
     """src/fri/fri_commit.rs:137-163 over the device-resident layers/trees:
     per layer send value, path, sibling value, sibling path (a 1-element
     layer first sends its value, as the reference does)."""
-    for val, sval, path, spath in proof.ctx.decommit_query(index, proof.n_layers, proof.log_n):
+    for val, sval, path, spath in proof.ctx.decommit_query(index, proof.n_layers, proof.log_n, proof.generation):
         # the gather reads layers of 2^(log_n-k) >= 2 elements; a 1-element
         # layer (blowup 1) has idx = sib = 0 and empty paths
         if not path and not spath:
@@ -781,4 +805,4 @@ def _mirror_commit(res: CommitResult, ctx: Context, log_n: int, channel: Channel
     channel.proof.append(fv)
     channel.compressed_proof.append(fv)
     channel.state = bytes(res.channel_out.digest).hex() if res.channel_out.has_state else ""
-    return FRIProof(ctx, log_n, roots, betas, int(res.final_value), int(res.final_degree))
+    return FRIProof(ctx, log_n, roots, betas, int(res.final_value), int(res.final_degree), ctx.commit_info()[0])

@@ -406,6 +406,36 @@ def test_decommit_errors(ctx):
     assert ln.value == sum(64 * (7 - k) for k in range(5))     # ... but the size is reported (5 layers)
 
 
+def test_stale_proof_refused(ctx, oracle):
+    """A FRIProof reads its layers from the context; once a later commit has
+    replaced them (here a smaller codeword) its read-backs raise instead of
+    serving the other commit's data (fri_commit_info generation)."""
+    import fri_amd
+    c12 = oracle.splitmix64_field(12, 512)
+    p1 = fri_amd.fri_commit(c12, 12, fri_amd.Channel(), ctx=ctx)
+    l1 = p1.layer(1)
+    assert l1.size == 2048
+    g1 = ctx.commit_info()
+    p2 = fri_amd.fri_commit(oracle.splitmix64_field(10, 128), 10, fri_amd.Channel(), ctx=ctx)
+    assert ctx.commit_info()[0] > g1[0] and ctx.commit_info()[1:] == (10, p2.n_layers)
+    with pytest.raises(fri_amd.FriError) as e:
+        p1.layer(0)
+    assert e.value.code == fri_amd.FRI_ESTATE
+    with pytest.raises(fri_amd.FriError) as e:
+        fri_amd.decommit_fri(1, 4095, p1, fri_amd.Channel())
+    assert e.value.code == fri_amd.FRI_ESTATE
+    with pytest.raises(fri_amd.FriError) as e:
+        ctx.layer(0, 12)                                     # wrong codeword size for the resident commit
+    assert e.value.code == fri_amd.FRI_ESTATE
+    assert p2.layer(0).size == 1024
+    # the same polynomial again: the new proof serves, the old one stays refused
+    p3 = fri_amd.fri_commit(c12, 12, fri_amd.Channel(), ctx=ctx)
+    assert np.array_equal(p3.layer(1), l1)
+    with pytest.raises(fri_amd.FriError):
+        p2.layer(0)
+
+
+
 # ---- trace side of the prover: fri_trace_commit (SURVEY §8(f) rank 2) -------
 def _stark101_trace(n):
     """STARK-101's FibonacciSq trace: a0 = 1, a1 = 3141592, a_{i+2} = a_{i+1}^2 + a_i^2 (mod p)."""

@@ -121,6 +121,11 @@ def test_composition_detects_constraint_violation(ctx):
     with pytest.raises(fri_amd.FriError) as e:
         ctx.fibsq_composition_commit(log_t, lb, (int(trace[-1]) + 1) % P, [1, 2, 3], channel_state=bytes(32))
     assert e.value.code == fri_amd.FRI_EDEGREE
+    # the refused commit's layers are not served afterwards
+    assert ctx.commit_info()[1:] == (0, 0)
+    buf = np.zeros(16, dtype=np.uint32)
+    assert ctx.lib.fri_layer_copy(ctx.h, 0, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                  buf.size) == fri_amd.FRI_ESTATE
     res = ctx.fibsq_composition_commit(log_t, lb, int(trace[-1]), [1, 2, 3], channel_state=bytes(32))
     assert res.n_rounds == log_t + 1
 

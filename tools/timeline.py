@@ -29,7 +29,7 @@ def main():
     first = [i for i, r in enumerate(rows) if r[2].startswith("k_ntt_pass") and r[2].split(",")[2].strip() == "true"]
     min_us = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0      # layer-0 leaf duration filter
     l0 = [i for i, r in enumerate(rows)
-          if r[2].startswith("k_layer_leaf<false, true>") and (r[1] - r[0]) / 1e3 >= min_us]
+          if r[2].startswith("k_layer_leaf<false, true") and (r[1] - r[0]) / 1e3 >= min_us]
     anchor = l0[-which]
     lo = max(i for i in first if i < anchor)
     later = [i for i in first if i > anchor]
