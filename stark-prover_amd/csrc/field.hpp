@@ -26,27 +26,33 @@ constexpr uint32_t R_MOD_P = 0x3FFFFFFFu;    // 2^32 mod p
 constexpr uint32_t R2_MOD_P = (uint32_t)(((unsigned __int128)1 << 64) % P);   // 2^64 mod p
 static_assert((uint32_t)(P * PINV) == 1u, "PINV");
 
-// Montgomery reduction of t < p^2: returns t * 2^-32 mod p, canonical.
+// Montgomery reduction of t < p * 2^32: returns t * 2^-32 mod p, canonical.
+// m = tlo * PINV is tlo + (tlo << 30) (PINV = 2^30 + 1: one v_lshl_add).
+// The borrow of hi(t) - hi(m*p) comes straight from v_sub_co_u32 (VCC):
+// written as __builtin_usub_overflow the compiler no longer widens the
+// compare to 64 bits (3 half-rate + 3 full-rate VALU per product).
 FRI_HD uint32_t redc(uint64_t t) {
     uint32_t tlo = (uint32_t)t, thi = (uint32_t)(t >> 32);
     uint32_t m = tlo * PINV;
     uint32_t u = (uint32_t)(((uint64_t)m * P) >> 32);
-    uint32_t r = thi - u;
-    return thi < u ? r + P : r;
+    uint32_t r;
+    const bool borrow = __builtin_usub_overflow(thi, u, &r);
+    return borrow ? r + P : r;
 }
 
 // a (canonical or Montgomery) x b (Montgomery) -> a*b*R^-1*R ... i.e.
 //   mmul(std, mont) = std product;  mmul(mont, mont) = mont product.
 FRI_HD uint32_t mmul(uint32_t a, uint32_t b) { return redc((uint64_t)a * b); }
 
-FRI_HD uint32_t add(uint32_t a, uint32_t b) {
-    uint32_t s = a + b;
-    return (s < a || s >= P) ? s - P : s;
-}
+// a - b for a < p, b <= p: one borrow-producing subtract, +p on borrow.
 FRI_HD uint32_t sub(uint32_t a, uint32_t b) {
-    uint32_t d = a - b;
-    return a < b ? d + P : d;
+    uint32_t d;
+    const bool borrow = __builtin_usub_overflow(a, b, &d);
+    return borrow ? d + P : d;
 }
+// a + b = a - (p - b): p > 2^31, so a + b can carry out of 32 bits; the
+// subtract form needs no carry test and no 64-bit compare.
+FRI_HD uint32_t add(uint32_t a, uint32_t b) { return sub(a, P - b); }
 FRI_HD uint32_t neg(uint32_t a) { return a ? P - a : 0u; }
 
 FRI_HD uint32_t to_mont(uint32_t a) { return mmul(a, R2_MOD_P); }

@@ -40,7 +40,11 @@ __device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4);
 #define NTT_TPB 512          // threads per NTT tile (16 elements each; 512: 128-byte row runs)
 #endif
 
-template <int A, int B, bool FIRST, int TPB>
+// Z (FIRST only): the input has d <= n / 2^Z coefficients, so after the
+// bit-reversal gather every row q with q mod 2^Z != 0 is zero and DIT stages
+// 0..Z-1 only copy a row into its zero partners (u + w*0 = u - w*0 = u):
+// they become register copies (an LDE of blowup 8 skips 3 of its log_n stages).
+template <int A, int B, bool FIRST, int TPB, int Z = 0>
 __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d, uint32_t* dst,
                                                   uint32_t log_n, uint32_t s0, const uint32_t* __restrict__ tw,
                                                   const uint32_t* __restrict__ pre_lo, const uint32_t* __restrict__ pre_hi,
@@ -102,18 +106,23 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
         return FIRST ? w : mmul(w, wl[t]);
     };
     // ---- phase A: stages 0..A-1 on 16 consecutive elements ----------------
+    static_assert(Z == 0 || (FIRST && Z <= A), "trivial stages only in the first pass, inside phase A");
 #pragma unroll
-    for (int e = 0; e < 16; e++) r[e] = lds[ntt_laddr(tid * 16 + e)];
+    for (int e = 0; e < 16; e++) r[e] = (e & ((1 << Z) - 1)) ? 0u : lds[ntt_laddr(tid * 16 + e)];
+#pragma unroll
+    for (int e = 0; e < 16; e++) r[e] = r[e & ~((1 << Z) - 1)];       // stages 0..Z-1
     {
         const uint32_t x0 = tid * 16;
 #pragma unroll
-        for (int t = 0; t < A; t++) {
+        for (int t = Z; t < A; t++) {
 #pragma unroll
             for (int e = 0; e < 16; e++) {
                 if (e & (1 << t)) continue;
                 const uint32_t q0 = (x0 + e) & (P - 1);
-                const uint32_t w = twid(t, q0);
-                const uint32_t u = r[e], v = mmul(r[e + (1 << t)], w);
+                // first pass: row q0 = x0 + e with x0 a multiple of 16, so the
+                // twiddle w_{2^(t+1)}^(e mod 2^t) is 1 at e mod 2^t == 0
+                const bool one = FIRST && (e & ((1 << t) - 1)) == 0;
+                const uint32_t u = r[e], v = one ? r[e + (1 << t)] : mmul(r[e + (1 << t)], twid(t, q0));
                 r[e] = add(u, v);
                 r[e + (1 << t)] = sub(u, v);
             }
@@ -182,7 +191,7 @@ __global__ void k_ntt_one(const uint32_t* src, size_t d, uint32_t* dst, const ui
     dst[0] = v;
 }
 
-template <bool FIRST>
+template <bool FIRST, int Z = 0>
 static void launch_pass(uint32_t ns, const uint32_t* src, size_t d, uint32_t* dst, uint32_t log_n, uint32_t s0,
                         const NttPlan& p, bool last, hipStream_t s) {
     const size_t n = (size_t)1 << log_n;
@@ -194,8 +203,8 @@ static void launch_pass(uint32_t ns, const uint32_t* src, size_t d, uint32_t* ds
     const uint32_t* qhi = last ? p.post_hi : nullptr;
 #define NTT_CASE(NSV, AV, BV)                                                                                   \
     case NSV:                                                                                                   \
-        hipLaunchKernelGGL((k_ntt_pass<AV, BV, FIRST, TPB>), dim3(blocks), dim3(TPB), 0, s, src, d, dst, log_n, s0, p.tw, \
-                           plo, phi, qlo, qhi);                                                                 \
+        hipLaunchKernelGGL((k_ntt_pass<AV, BV, FIRST, TPB, (Z < AV ? Z : AV)>), dim3(blocks), dim3(TPB), 0, s, src, d, \
+                           dst, log_n, s0, p.tw, plo, phi, qlo, qhi);                                           \
         break;
     switch (ns) {
         NTT_CASE(1, 1, 0) NTT_CASE(2, 2, 0) NTT_CASE(3, 3, 0) NTT_CASE(4, 4, 0)
@@ -203,6 +212,20 @@ static void launch_pass(uint32_t ns, const uint32_t* src, size_t d, uint32_t* ds
         default: break;
     }
 #undef NTT_CASE
+}
+
+// First pass with the zero rows of a padded input skipped: z trivial stages
+// when d <= n / 2^z (z <= 3, and at most the pass's phase-A stages).
+static void launch_first(uint32_t ns, const uint32_t* src, size_t d, uint32_t* dst, uint32_t log_n, const NttPlan& p,
+                         bool last, hipStream_t s) {
+    uint32_t z = 0;
+    while (z < 3 && z < ns && ((size_t)d << (z + 1)) <= ((size_t)1 << log_n)) z++;
+    switch (z) {
+        case 0: launch_pass<true, 0>(ns, src, d, dst, log_n, 0, p, last, s); break;
+        case 1: launch_pass<true, 1>(ns, src, d, dst, log_n, 0, p, last, s); break;
+        case 2: launch_pass<true, 2>(ns, src, d, dst, log_n, 0, p, last, s); break;
+        default: launch_pass<true, 3>(ns, src, d, dst, log_n, 0, p, last, s); break;
+    }
 }
 
 void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, hipStream_t s) {
@@ -213,7 +236,7 @@ void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, 
     }
     uint32_t first = log_n % 8;
     if (first == 0) first = 8;
-    launch_pass<true>(first, src, d, dst, log_n, 0, p, first == log_n, s);
+    launch_first(first, src, d, dst, log_n, p, first == log_n, s);
     for (uint32_t s0 = first; s0 < log_n; s0 += 8)
         launch_pass<false>(8, dst, 0, dst, log_n, s0, p, s0 + 8 == log_n, s);
 }
