@@ -40,6 +40,18 @@ def test_cpp_host_mirror_cpu():
     assert "ok   cpu::verify_fibsq_accepts_and_rejects" in out
 
 
+def test_device_field_arithmetic_on_host(tmp_path):
+    """csrc/field.hpp (redc / add / sub / Montgomery conversions used by every
+    kernel) is host-callable: check it against __int128 arithmetic on edge
+    values (0, 1, p-1, 2^31, ...) and 2M random operand pairs
+    (tests/cpp/test_field.cpp)."""
+    exe = tmp_path / "test_field"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-o", str(exe),
+                    os.path.join(ROOT, "tests", "cpp", "test_field.cpp")], check=True, timeout=300)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and " 0 failures" in p.stdout, p.stdout
+
+
 def test_host_library_exports_reference_api():
     _build()
     syms = subprocess.run(["nm", "-DC", "--defined-only", os.path.join(PKG, "lib", "libstark101.so")],
