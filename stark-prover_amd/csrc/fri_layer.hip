@@ -141,7 +141,7 @@ __device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32
     m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
     const uint32_t wave = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) { red[3 * wave] = m0; red[3 * wave + 1] = m1; red[3 * wave + 2] = m2; }
-    __syncthreads();
+    lds_barrier();          // red[] only: the leaf digest stores need not drain here
     if (threadIdx.x == 0) {
         int a = -1, b = -1, c = -1;
         for (uint32_t i = 0; i < blockDim.x / 64; i++) { a = max(a, red[3 * i]); b = max(b, red[3 * i + 1]); c = max(c, red[3 * i + 2]); }
@@ -226,6 +226,12 @@ __global__ __launch_bounds__(TPB) void k_layer_leaf(LayerTask t) {
                         tr + 8 * level_offset(L, 4), (size_t)blockIdx.x * TPB);
 }
 
+// Levels of the wide leaf kernel with fewer than WIDE_PAIR_MAX nodes in the
+// whole layer are latency-bound: they use the lane-pair node.
+#ifndef WIDE_PAIR_MAX
+#define WIDE_PAIR_MAX (1u << 16)
+#endif
+
 // Wide leaf kernel for narrow layers (2^10 .. 2^18 elements): one leaf per
 // lane, 256 leaves per workgroup, levels 1..4 through LDS (one node per lane
 // per level): latency 1 leaf + 4 nodes instead of the quad form's 4 + 5.
@@ -255,16 +261,20 @@ __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
     if (COMMIT) coef_task(t, blockIdx.x, gridDim.x, red);
     lds_barrier();
     uint32_t cnt = 256;
+    const shaq::Role qr = shaq::role_of(threadIdx.x);
 #pragma unroll 1
     for (uint32_t j = 1; j <= 4; j++) {
         cnt >>= 1;
-        if (threadIdx.x < cnt) {
+        uint32_t* out = tr + 8 * (level_offset(L, j) + ((size_t)blockIdx.x << (8 - j)));
+        if ((size_t)cnt * gridDim.x < WIDE_PAIR_MAX) {
+            pair_level(A, B, out, threadIdx.x, cnt, qr);   // latency-bound level: node per lane pair
+        } else if (threadIdx.x < cnt) {
             Dg a, b, o;
             dg_lds_load(A + 4 * threadIdx.x, a);
             dg_lds_load(A + 4 * threadIdx.x + 2, b);
             hnode(a, b, o);
             dg_lds_store(B + 2 * threadIdx.x, o);
-            dg_store(tr + 8 * (level_offset(L, j) + ((size_t)blockIdx.x << (8 - j)) + threadIdx.x), o);
+            dg_store(out + 8 * threadIdx.x, o);
         }
         lds_barrier();
         uint4* tmp = A; A = B; B = tmp;
@@ -513,7 +523,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
             if ((tid & 63) == 0) { red[3 * (tid >> 6)] = m0; red[3 * (tid >> 6) + 1] = m1; red[3 * (tid >> 6) + 2] = m2; }
         }
     }
-    __syncthreads();
+    lds_barrier();
     // ---- degree of poly_k (reference degree field; see DevState), uniform ----
     int deg = -1;
     if (COMMIT) {
