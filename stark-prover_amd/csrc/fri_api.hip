@@ -558,6 +558,24 @@ static uint32_t* coef_buf(Plan& p, int r) {
     return (r % 2 == 1) ? p.coefA : p.coefB;
 }
 
+// Layer k of the resident plan as a commit-mode LayerTask.
+static LayerTask commit_task(fri_ctx* ctx, int k) {
+    Plan& p = ctx->plan;
+    LayerTask t{};
+    t.prev = k ? p.layers + p.layer_off[k - 1] : nullptr;
+    t.xinv = k ? p.xinv + p.xinv_off[k - 1] : nullptr;
+    t.values = p.layers + p.layer_off[k];
+    t.tree = p.trees + p.tree_off[k];
+    t.L = p.log_n - (uint32_t)k;
+    t.k = k;
+    t.coef_in = k ? coef_buf(p, k - 1) : p.d_in;
+    t.coef_out = k ? coef_buf(p, k) : nullptr;
+    t.d0 = p.d;
+    t.wgmax = p.wgmax;
+    t.st = ctx->d_state;
+    return t;
+}
+
 // Enqueue the whole commit on ctx->stream (captured into a graph or eager):
 // LDE, then per layer k = 0..rmax one launch_layer (gated on the device).
 static void enqueue_commit(fri_ctx* ctx) {
@@ -573,6 +591,16 @@ static void enqueue_commit(fri_ctx* ctx) {
     span_end(ctx, sp);
     for (int k = 0; k <= p.rmax; k++) {
         const uint32_t L = log_n - (uint32_t)k;
+        if (L <= TOP_LOG) {
+            // the remaining small layers: one single-workgroup launch
+            LayerTask ts[TOP_LOG + 1];
+            uint32_t nt = 0;
+            for (int kk = k; kk <= p.rmax; kk++) ts[nt++] = commit_task(ctx, kk);
+            size_t spk = span_begin(ctx, k == 0 ? "layer0" : "layers", 0);
+            launch_tail(ts, nt, s);
+            span_end(ctx, spk);
+            break;
+        }
         LayerTask t{};
         t.prev = k ? p.layers + p.layer_off[k - 1] : nullptr;
         t.xinv = k ? p.xinv + p.xinv_off[k - 1] : nullptr;
@@ -1339,19 +1367,14 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
             FRI_HIP(ctx, hipMemcpyAsync(p.layers + p.layer_off[k] + (size_t)block_of[r] * B, db.gath + (size_t)r * B,
                                         B * 4, hipMemcpyDeviceToDevice, s));
         for (int kk = k + 1; kk <= p.rmax; kk++) {
-            LayerTask t{};
-            t.prev = p.layers + p.layer_off[kk - 1];
-            t.xinv = p.xinv + p.xinv_off[kk - 1];
-            t.values = p.layers + p.layer_off[kk];
-            t.tree = p.trees + p.tree_off[kk];
-            t.L = log_n - (uint32_t)kk;
-            t.k = kk;
-            t.coef_in = coef_buf(p, kk - 1);
-            t.coef_out = coef_buf(p, kk);
-            t.d0 = d;
-            t.wgmax = p.wgmax;
-            t.st = ctx->d_state;
-            launch_layer(t, s);
+            if (log_n - (uint32_t)kk <= TOP_LOG) {       // small layers: one launch
+                LayerTask ts[TOP_LOG + 1];
+                uint32_t nt = 0;
+                for (int k2 = kk; k2 <= p.rmax; k2++) ts[nt++] = commit_task(ctx, k2);
+                launch_tail(ts, nt, s);
+                break;
+            }
+            launch_layer(commit_task(ctx, kk), s);
         }
         span_end(ctx, sp);
         break;

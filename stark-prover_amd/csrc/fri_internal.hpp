@@ -102,6 +102,9 @@ struct LayerTask {
     int gidx;                  //   layers): skip when !gst->active[gidx]
 };
 void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end = nullptr);
+// Layers ts[0..n) (consecutive, 2^L <= 2^TOP_LOG elements, commit mode) in
+// one single-workgroup launch (k_tree_tail), n <= TOP_LOG + 1.
+void launch_tail(const LayerTask* ts, uint32_t n, hipStream_t s);
 // Coefficient task of layer t.k alone (grid G): k == 0 scans the input for
 // deg_0, k >= 1 folds poly_{k-1} -> poly_k; maxima into t.wgmax[3*G].
 void launch_coef(const LayerTask& t, uint32_t G, hipStream_t s);

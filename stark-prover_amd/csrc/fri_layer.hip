@@ -627,6 +627,193 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     }
 }
 
+// ------------------------------------------------------------- tail ----
+// The last layers of a commit (2^L <= 2^TOP_LOG elements each) in ONE
+// workgroup and ONE launch: per layer the body of k_tree_top<true, *, true>
+// (fold, leaves, coefficient fold, degree, tree levels, channel step), with
+// the layer values, the coefficients, beta, the degree and the gate handed to
+// the next layer through LDS.  Saves per layer a kernel boundary, the HBM
+// round trip of the folded values and coefficients, and the cold first level
+// of a fresh workgroup.  The channel state stays in wave 7's registers.
+struct TailTask {
+    LayerTask t[TOP_LOG + 1];   // consecutive layers k0 .. k0 + n - 1 (commit mode)
+    uint32_t n;
+};
+
+template <bool FOLD0>
+__global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
+    const LayerTask& t0 = tt.t[0];
+    if (gated_off(t0)) return;
+    __shared__ uint4 lds[2 * 512 + 2 * 256];
+    __shared__ uint32_t vals[2][512];          // this / previous layer's values
+    __shared__ uint32_t coefs[2][512];         // this / previous round's polynomial
+    __shared__ int32_t red[24];
+    __shared__ uint32_t s_beta_m, s_active;
+    __shared__ int32_t s_deg;
+    const uint32_t tid = threadIdx.x;
+    const bool chan_wave = tid >= 448;
+    DevState* st = t0.st;
+    uint32_t cs[8], X[4];
+    uint32_t has = 0;
+    if (chan_wave) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) cs[i] = st->chan[i];
+        has = st->chan_has;
+    }
+    uint32_t pending = chan_wave ? st->chan_pending : 0u;
+    if (tid >= 384 && tid < 448) kcache_touch_sha_tables();
+    uint32_t beta_m = FOLD0 ? st->beta_mont[t0.k - 1] : 0u;
+    int prev_deg = FOLD0 ? st->deg[t0.k - 1] : -1;
+    const shaq::Role R = shaq::role_of(tid);
+#pragma unroll 1
+    for (uint32_t li = 0; li < tt.n; li++) {
+        const LayerTask& t = tt.t[li];
+        const int k = t.k;
+        const uint32_t L = t.L, N = 1u << L;
+        const bool fold = FOLD0 || li > 0;
+        uint32_t* cur_v = vals[li & 1];
+        const uint32_t* prev_v = vals[(li & 1) ^ 1];
+        uint32_t* cur_c = coefs[li & 1];
+        const uint32_t* prev_c = coefs[(li & 1) ^ 1];
+        uint4* A = lds;
+        uint4* B = lds + 2 * 512;
+        uint32_t* tr = t.tree;
+        // ---- fold + leaves (spare lanes of wave 0 recompute leaf i mod N) ----
+        for (uint32_t i = tid; i < max(N, 64u); i += blockDim.x) {
+            const uint32_t j = i & (N - 1);
+            const bool real = i < N;
+            uint32_t v;
+            if (fold) {
+                const uint32_t a = li ? prev_v[j] : t.prev[j], b = li ? prev_v[j + N] : t.prev[j + N];
+                v = fold1(a, b, t.xinv[j], beta_m);
+                if (real) t.values[j] = v;
+            } else {
+                v = t.values[j];
+            }
+            if (real) cur_v[j] = v;
+            Dg d;
+            cleaf(v, d);
+            if (real) {
+                dg_store(tr + 8 * j, d);
+                dg_lds_store(A + 2 * j, d);
+            }
+        }
+        // ---- coefficient fold of round k-1 (or the input scan at k == 0) ----
+        int m0 = -1, m1 = -1, m2 = -1;
+        if (k == 0) {
+            for (size_t j = tid; j < t.d0; j += blockDim.x)
+                if (t.coef_in[j]) m0 = max(m0, (int)j);
+        } else {
+            const uint32_t len = (uint32_t)(prev_deg + 1), nlen = (len + 1) / 2;
+            const bool in_lds = li > 0 && k >= 2;      // poly_{k-1} was folded by this kernel
+            for (uint32_t j = tid; j < nlen; j += blockDim.x) {
+                const uint32_t e = in_lds ? prev_c[2 * j] : t.coef_in[2 * j];
+                const uint32_t o = (2 * j + 1 < len) ? (in_lds ? prev_c[2 * j + 1] : t.coef_in[2 * j + 1]) : 0u;
+                const uint32_t v = add(e, mmul(o, beta_m));
+                cur_c[j] = v;
+                if (v) m0 = (int)j;
+                if (e) m1 = (int)j;
+                if (o) m2 = (int)j;
+            }
+        }
+        m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
+        if ((tid & 63) == 0) { red[3 * (tid >> 6)] = m0; red[3 * (tid >> 6) + 1] = m1; red[3 * (tid >> 6) + 2] = m2; }
+        lds_barrier();
+        int deg;
+        {
+            int a = -1, b = -1, c = -1;
+#pragma unroll
+            for (int i = 0; i < 8; i++) { a = max(a, red[3 * i]); b = max(b, red[3 * i + 1]); c = max(c, red[3 * i + 2]); }
+            deg = (k == 0) ? a : (b < 0 ? c : a);
+        }
+        const bool is_final = deg < 1;
+        const int job_end = is_final ? CJ_END_FINAL : CJ_END_ROUND;
+        uint32_t fv = 0;                               // fri_commit.rs:109-113
+        if (chan_wave && is_final && deg == 0) fv = (k == 0) ? t.coef_in[0] : cur_c[0];
+        // ---- levels + channel jobs (k_tree_top) ----
+        int job = CJ_END_FINAL;
+        if (chan_wave) job = !has ? CJ_ROOT : (pending ? CJ_REHASH : CJ_MID);
+        const uint32_t nlev = L;
+        // uniform count of loop iterations: the channel prework count is the
+        // same on every lane (has / pending follow the layer index)
+        const uint32_t npre_u = (li == 0) ? (!st->chan_has ? 0u : (st->chan_pending ? 3u : 1u)) : 3u;
+        const uint32_t pre_in_levels = min(npre_u, min(nlev, 8u));
+        const uint32_t total = nlev + (npre_u - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
+        uint32_t cnt = N;
+#pragma unroll 1
+        for (uint32_t it = 0; it < total; it++) {
+            const bool level = it < nlev;
+            if (level) {
+                cnt >>= 1;
+                uint32_t* out = tr + 8 * level_offset(L, 1 + it);
+                if (cnt <= 128) {
+                    pair_level(A, B, out, tid, cnt, R);
+                } else {
+#pragma unroll 1
+                    for (uint32_t q = tid; q < cnt; q += blockDim.x) {
+                        Dg a, b, o;
+                        dg_lds_load(A + 4 * q, a);
+                        dg_lds_load(A + 4 * q + 2, b);
+                        cnode(a, b, o);
+                        dg_lds_store(B + 2 * q, o);
+                        dg_store(out + 8 * q, o);
+                    }
+                }
+            }
+            if (chan_wave && job < job_end && (level ? (cnt <= 192 && job < CJ_ROOT) : true)) {
+                chan_job(job, cs, X, has, A, fv, R);
+                job++;
+            }
+            lds_barrier();
+            if (level) { uint4* tmp = A; A = B; B = tmp; }
+        }
+        // ---- results (one lane of wave 7), hand-off to the next layer ----
+        if (tid == 448) {
+            st->deg[k] = deg;
+            Dg root;
+            dg_lds_load(A, root);
+#pragma unroll
+            for (int i = 0; i < 8; i++) st->roots[k][i] = root.w[i];
+            st->n_layers = (uint32_t)k + 1;
+            uint32_t active = 0, bm = 0;
+            if (deg >= 1 && k < MAXR && L >= 1) {
+                uint32_t beta = chan_beta(cs);
+#pragma unroll
+                for (int i = 0; i < 8; i++) st->chan[i] = cs[i];
+                st->chan_has = 1;
+                st->chan_pending = 1;                    // receive's rehash deferred to the next layer
+                if (st->forced) beta = st->forced_beta[k];
+                st->beta[k] = beta;
+                bm = to_mont(beta);
+                st->beta_mont[k] = bm;
+                st->active[k] = 1;
+                st->n_rounds = (uint32_t)k + 1;
+                active = 1;
+            } else {
+                st->active[k] = 0;
+                if (deg >= 1) {
+                    st->status = 7u;                     // FRI_EDEGREE
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) st->chan[i] = cs[i];   // after send(final.to_bytes())
+                    st->final_value = fv;
+                    st->final_degree = deg;
+                    st->chan_has = 1;
+                    st->chan_pending = 0;
+                }
+            }
+            s_beta_m = bm;
+            s_active = active;
+            s_deg = deg;
+        }
+        if (chan_wave) { has = 1; pending = 1; }
+        lds_barrier();
+        if (!s_active) break;                            // uniform
+        beta_m = s_beta_m;
+        prev_deg = s_deg;
+    }
+}
+
 // ------------------------------------------------------------ launcher ----
 // Layer schedule (levels are consumed 4 at a time):
 //   L <= 9 : one k_tree_top from the leaves.
@@ -709,6 +896,15 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
     }
     if (commit) hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, mx, G);
     else hipLaunchKernelGGL((k_tree_top<false, false, false>), dim3(1), dim3(512), 0, s, t, l, nomx, G);
+}
+
+void launch_tail(const LayerTask* ts, uint32_t n, hipStream_t s) {
+    TailTask tt{};
+    tt.n = n;
+    for (uint32_t i = 0; i < n; i++) tt.t[i] = ts[i];
+    tt.t[0] = with_gate(ts[0]);
+    if (ts[0].prev) hipLaunchKernelGGL((k_tree_tail<true>), dim3(1), dim3(512), 0, s, tt);
+    else hipLaunchKernelGGL((k_tree_tail<false>), dim3(1), dim3(512), 0, s, tt);
 }
 
 __global__ __launch_bounds__(256) void k_coef(LayerTask t) {
