@@ -339,6 +339,44 @@ __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L
     }
 }
 
+// Eight tree levels in one launch for the narrow part of a large layer:
+// 256 level-l digests per workgroup -> 1 level-(l+8) digest, every level on
+// lane pairs (level 1 reads its children straight from HBM).  Replaces two
+// k_tree_mid<256> launches: one kernel boundary, one HBM round trip of the
+// level-(l+4) digests and one cold start less per layer.
+__global__ __launch_bounds__(256) void k_tree_mid8(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st,
+                                                   int gate, const int32_t* mx_in, int32_t* mx_out, uint32_t R) {
+    if (st && gate >= 0 && !st->active[gate]) return;
+    __shared__ uint4 lds[256 + 128];
+    uint4* A = lds;
+    uint4* B = lds + 256;
+    const uint32_t t = threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * 256;
+    const uint32_t* in = tree + 8 * level_offset(L, l);
+    const shaq::Role qr = shaq::role_of(t);
+    {
+        const uint32_t q = t >> 1, half = (t & 1u) ^ 1u;
+        Dg a, b;
+        dg_load(in + 8 * (base + 2 * q), a);
+        dg_load(in + 8 * (base + 2 * q + 1), b);
+        if (mx_in) reduce_mx(mx_in, mx_out, blockIdx.x, R);
+        uint32_t o[4];
+        shaq::node(a.w, b.w, o, qr);
+        const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
+        A[2 * q + half] = v;
+        reinterpret_cast<uint4*>(tree + 8 * (level_offset(L, l + 1) + (base >> 1) + q))[half] = v;
+    }
+    lds_barrier();
+    uint32_t cnt = 128;
+#pragma unroll 1
+    for (uint32_t j = 2; j <= 8; j++) {
+        cnt >>= 1;
+        pair_level(A, B, tree + 8 * (level_offset(L, l + j) + (base >> j)), t, cnt, qr);
+        lds_barrier();
+        uint4* tmp = A; A = B; B = tmp;
+    }
+}
+
 // One scalar load per 64-byte line of every __constant__ table the compact
 // SHA forms read (KTAB, PAD_KW_C, PAD_KW_1024, PAD_KW_1536, 256 B each):
 // fills the CU's scalar cache while the inputs load, instead of cold misses
@@ -826,6 +864,9 @@ static LayerTask with_gate(const LayerTask& in) {
     return t;
 }
 
+#ifndef MID8
+#define MID8 1               // k_tree_mid8 for the narrow levels of large layers
+#endif
 #ifndef QUAD_TPB
 #define QUAD_TPB 256         // quad leaf kernel: threads per WG (1024 leaves per WG)
 #endif
@@ -885,14 +926,19 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
         const uint32_t grid = (uint32_t)(nodes / nin);
         const uint32_t R = nin / out_per_wg;
         int32_t* mx_out = commit ? t.wgmax + mx_off : nullptr;
+        // eight narrow levels in one launch when four would leave more than
+        // the top takes (L - l >= 14: two k_tree_mid<256> otherwise)
+        const bool eight = nin == 256 && L - l >= 8 + 6 && MID8;
         if (nin == 1024)
             hipLaunchKernelGGL((k_tree_mid<1024>), dim3(grid), dim3(512), 0, s, t.tree, L, l, t.gst, gate, mx, mx_out, R);
+        else if (eight)
+            hipLaunchKernelGGL(k_tree_mid8, dim3(grid), dim3(256), 0, s, t.tree, L, l, t.gst, gate, mx, mx_out, R);
         else
             hipLaunchKernelGGL((k_tree_mid<256>), dim3(grid), dim3(128), 0, s, t.tree, L, l, t.gst, gate, mx, mx_out, R);
         if (commit) { mx = mx_out; mx_off += 3 * (size_t)grid; }
         G = grid;
-        out_per_wg = nin / 16;
-        l += 4;
+        out_per_wg = eight ? 1u : nin / 16;
+        l += eight ? 8u : 4u;
     }
     if (commit) hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, mx, G);
     else hipLaunchKernelGGL((k_tree_top<false, false, false>), dim3(1), dim3(512), 0, s, t, l, nomx, G);
