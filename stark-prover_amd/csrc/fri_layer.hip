@@ -232,6 +232,10 @@ __global__ __launch_bounds__(TPB) void k_layer_leaf(LayerTask t) {
 #define WIDE_PAIR_MAX (1u << 16)
 #endif
 
+// Tree levels the wide leaf kernel builds: all 8 of its 256-leaf subtree when
+// the rest of the layer then fits the single-workgroup top (no mid launch).
+__host__ __device__ __forceinline__ uint32_t wide_levels(uint32_t L) { return L <= 8 + TOP_LOG ? 8u : 4u; }
+
 // Wide leaf kernel for narrow layers (2^10 .. 2^18 elements): one leaf per
 // lane, 256 leaves per workgroup, levels 1..4 through LDS (one node per lane
 // per level): latency 1 leaf + 4 nodes instead of the quad form's 4 + 5.
@@ -262,8 +266,9 @@ __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
     lds_barrier();
     uint32_t cnt = 256;
     const shaq::Role qr = shaq::role_of(threadIdx.x);
+    const uint32_t nlev = wide_levels(L);
 #pragma unroll 1
-    for (uint32_t j = 1; j <= 4; j++) {
+    for (uint32_t j = 1; j <= nlev; j++) {
         cnt >>= 1;
         uint32_t* out = tr + 8 * (level_offset(L, j) + ((size_t)blockIdx.x << (8 - j)));
         if ((size_t)cnt * gridDim.x < WIDE_PAIR_MAX) {
@@ -905,7 +910,7 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
         }
     } else {
         G = 1u << (L - 8);
-        out_per_wg = 16;
+        out_per_wg = 256u >> wide_levels(L);
         if (fold) {
             if (commit) hipLaunchKernelGGL((k_layer_leaf_wide<true, true>), dim3(G), dim3(256), 0, s, t);
             else hipLaunchKernelGGL((k_layer_leaf_wide<true, false>), dim3(G), dim3(256), 0, s, t);
@@ -919,7 +924,7 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
     // coefficient maxima: level 0 at wgmax[0 .. 3G); each mid reduces R producers per WG
     const int32_t* mx = commit ? t.wgmax : nullptr;
     size_t mx_off = 3 * (size_t)G;
-    uint32_t l = 4;
+    uint32_t l = L >= QUAD_MIN_LOG ? 4u : wide_levels(L);
     while (L - l > TOP_LOG) {
         const size_t nodes = (size_t)1 << (L - l);
         const uint32_t nin = nodes >= ((size_t)1 << 18) ? 1024u : 256u;
