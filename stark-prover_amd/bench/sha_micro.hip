@@ -83,6 +83,61 @@ __global__ __launch_bounds__(256, LB) void k_node_x2(const uint4* __restrict__ i
     }
 }
 
+// ---- issue-mix probe: the unrolled node with every add as a separate
+// full-rate v_add_u32 (inline asm, so the compiler cannot re-form v_add3):
+// 17 instead of 14 instructions per round, but 11 of them full rate.
+__device__ __forceinline__ uint32_t vadd(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t kadd(uint32_t k, uint32_t b) {
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %2" : "=v"(r) : "s"(k), "v"(b));
+    return r;
+}
+__device__ __forceinline__ void rounds_noadd3(uint32_t st[8], uint32_t w[16], bool pad) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int t = 0; t < 64; t++) {
+        uint32_t kw;
+        if (pad) {
+            kw = kadd(shaf::PAD_KW.kw[t], 0u * h + h) ; // h + KW
+        } else {
+            uint32_t wt;
+            if (t < 16) wt = w[t];
+            else {
+                wt = vadd(vadd(vadd(w[t & 15], shaf::s0(w[(t - 15) & 15])), w[(t - 7) & 15]), shaf::s1(w[(t - 2) & 15]));
+                w[t & 15] = wt;
+            }
+            kw = vadd(kadd(sha::K(t), wt), h);
+        }
+        const uint32_t t1 = vadd(vadd(kw, shaf::S1(e)), shaf::chf(e, f, g));
+        const uint32_t t2 = vadd(shaf::S0(a), shaf::majf(a, b, c));
+        h = g; g = f; f = e; e = vadd(d, t1); d = c; c = b; b = a; a = vadd(t1, t2);
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+__device__ __forceinline__ void node_noadd3(const uint32_t* l, const uint32_t* r, uint32_t* o) {
+    uint32_t w[16];
+    for (int i = 0; i < 8; i++) { w[i] = l[i]; w[8 + i] = r[i]; }
+    sha::init(o);
+    rounds_noadd3(o, w, false);
+    rounds_noadd3(o, w, true);
+}
+template <int LB>
+__global__ __launch_bounds__(256, LB) void k_node_na3(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint4 a = in[4 * i], b = in[4 * i + 1], c = in[4 * i + 2], d = in[4 * i + 3];
+        uint32_t l[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t r[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+        uint32_t o[8];
+        node_noadd3(l, r, o);
+        out[2 * i] = make_uint4(o[0], o[1], o[2], o[3]);
+        out[2 * i + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+    }
+}
+
 
 // ---- VALU calibration: 16 independent chains per lane, OP per iteration
 template <int OP>
@@ -153,6 +208,8 @@ int main() {
     printf("node v2==v1: %d\n", memcmp(o1, o2, n * 32) == 0);
     hipLaunchKernelGGL((k_node_x2<1>), dim3(grid / 2), dim3(256), 0, 0, nin, out, n); CK(hipMemcpy(o2, out, n * 32, hipMemcpyDeviceToHost));
     printf("node x2==v1: %d\n", memcmp(o1, o2, n * 32) == 0);
+    hipLaunchKernelGGL((k_node_na3<1>), dim3(grid), dim3(256), 0, 0, nin, out, n); CK(hipMemcpy(o2, out, n * 32, hipMemcpyDeviceToHost));
+    printf("node no-add3==v1: %d\n", memcmp(o1, o2, n * 32) == 0);
     const double peak = 256.0 * 128 * 2.4e9;
     auto rep = [&](const char* name, float ms, double comps, double ops_per_comp) {
         double cps = comps / (ms * 1e-3);
@@ -168,6 +225,8 @@ int main() {
     rep("node v2 lb1", timeit([&] { hipLaunchKernelGGL((k_node<2, 1>), dim3(grid), dim3(256), 0, 0, nin, out, n); }, it), 2.0 * n, 1450);
     rep("node v2 lb4", timeit([&] { hipLaunchKernelGGL((k_node<2, 4>), dim3(grid), dim3(256), 0, 0, nin, out, n); }, it), 2.0 * n, 1450);
     rep("node v2 lb8", timeit([&] { hipLaunchKernelGGL((k_node<2, 8>), dim3(grid), dim3(256), 0, 0, nin, out, n); }, it), 2.0 * n, 1450);
+    rep("node no-add3 lb1", timeit([&] { hipLaunchKernelGGL((k_node_na3<1>), dim3(grid), dim3(256), 0, 0, nin, out, n); }, it), 2.0 * n, 1450);
+    rep("node no-add3 lb4", timeit([&] { hipLaunchKernelGGL((k_node_na3<4>), dim3(grid), dim3(256), 0, 0, nin, out, n); }, it), 2.0 * n, 1450);
     rep("node x2 lb1", timeit([&] { hipLaunchKernelGGL((k_node_x2<1>), dim3(grid / 2), dim3(256), 0, 0, nin, out, n); }, it), 2.0 * n, 1450);
     rep("node x2 lb4", timeit([&] { hipLaunchKernelGGL((k_node_x2<4>), dim3(grid / 2), dim3(256), 0, 0, nin, out, n); }, it), 2.0 * n, 1450);
     rep("node v2 lb1 grid2048", timeit([&] { hipLaunchKernelGGL((k_node<2, 1>), dim3(2048), dim3(256), 0, 0, nin, out, n); }, it), 2.0 * n, 1450);
