@@ -34,7 +34,15 @@ namespace fri {
 __device__ __forceinline__ uint32_t pow2lvl(const uint32_t* lo, const uint32_t* hi, size_t j, uint32_t v) {
     return mmul(mmul(v, hi[j >> POW_LO_LOG]), lo[j & ((1u << POW_LO_LOG) - 1)]);
 }
-__device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4); }
+// LDS word of tile element x.  One pad word per 16 keeps a thread's 16
+// consecutive elements (phase A) and the stride-16 groups (phase B) on 64
+// distinct banks; two more per 1024 spread the 32 columns of the load and
+// store phases (column stride 256 + 16 = 16 mod 64 banks alone: 8-way
+// conflicts, SQ_LDS_BANK_CONFLICT) over distinct banks.
+#ifndef NTT_PAD10
+#define NTT_PAD10 1
+#endif
+__device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4) + (NTT_PAD10 ? (x >> 10) << 1 : 0u); }
 
 #ifndef NTT_TPB
 #define NTT_TPB 512          // threads per NTT tile (16 elements each; 512: 128-byte row runs)
@@ -52,7 +60,7 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
                                                   const uint32_t* __restrict__ post_hi) {
     // tile: 16 elements per thread; C columns (C consecutive words per row)
     constexpr uint32_t NS = A + B, P = 1u << NS, TILE = 16u * TPB, C = TILE / P;
-    __shared__ uint32_t lds[TILE + TILE / 16];
+    __shared__ uint32_t lds[TILE + TILE / 16 + 2 * (TILE >> 10)];
     const uint32_t tid = threadIdx.x;
     const size_t ncols = ((size_t)1 << log_n) >> NS;
     const size_t col0 = (size_t)blockIdx.x * C;
