@@ -237,7 +237,11 @@ typedef struct {
     int (*sendrecv)(void* user, const void* send, void* recv, size_t bytes, int peer);
 } fri_collectives;
 
-/* RCCL transport (xGMI): rank 0 creates the id, the caller distributes it. */
+/* RCCL transport (xGMI): rank 0 creates the id, the caller distributes it.
+ * A rendezvous that does not complete within FRI_RCCL_TIMEOUT_S seconds
+ * (environment, default 120) returns FRI_ERCCL instead of blocking; a sharded
+ * commit whose collectives make no progress for that long aborts the
+ * communicators and returns FRI_ERCCL (the context then needs a new attach). */
 int fri_dist_unique_id(uint8_t uid[128]);
 int fri_dist_attach_rccl(fri_ctx* ctx, int rank, int world, const uint8_t uid[128]);
 /* Host-callback transport (e.g. torch.distributed gloo; used by tests). */

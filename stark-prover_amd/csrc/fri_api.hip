@@ -3,8 +3,14 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -989,14 +995,55 @@ static int tp_host_stage(fri_ctx* ctx, size_t bytes) {
     return FRI_OK;
 }
 
+// A rendezvous or collective that never completes (a peer that is gone, a
+// fabric that does not come up) ends in FRI_ERCCL after FRI_RCCL_TIMEOUT_S
+// seconds (default 120) instead of hanging the caller: the communicator setup
+// runs on a helper thread the attach waits for with that deadline, and the
+// sharded path's stream syncs poll with it and abort the communicators (which
+// ends RCCL kernels spinning on an absent peer).  The sharded bench then
+// falls back to independent commits.
+static double rccl_timeout_s() {
+    const char* e = getenv("FRI_RCCL_TIMEOUT_S");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0.0 ? v : 120.0;
+}
+static double seconds_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+static void rccl_abort(fri_ctx* ctx) {
+    Transport& tp = ctx->tp;
+    if (tp.xcomm) ncclCommAbort(tp.xcomm);
+    if (tp.comm) ncclCommAbort(tp.comm);
+    tp.comm = tp.xcomm = nullptr;      // the transport is gone: later sharded calls see FRI_ESTATE
+}
 #define FRI_NCCL(ctx, expr)                                                                  \
     do {                                                                                     \
-        ncclResult_t _r = (expr);                                                            \
-        if (_r != ncclSuccess) {                                                             \
-            (ctx)->err = std::string(#expr) + ": " + ncclGetErrorString(_r);                 \
-            return FRI_ERCCL;                                                                \
-        }                                                                                    \
+        const ncclResult_t _r = (expr);                                                      \
+        if (_r != ncclSuccess) return fail((ctx), FRI_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
     } while (0)
+
+// Stream sync of the sharded path with the same deadline: RCCL kernels whose
+// peer never arrives spin on the device; aborting the communicators ends them.
+static int sync_sharded(fri_ctx* ctx, hipStream_t s) {
+    if (ctx->tp.host || !ctx->tp.comm) {
+        FRI_HIP(ctx, hipStreamSynchronize(s));
+        return FRI_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    const double lim = rccl_timeout_s();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return FRI_OK;
+        if (e != hipErrorNotReady) FRI_HIP(ctx, e);
+        if (seconds_since(t0) > lim) {
+            rccl_abort(ctx);
+            (void)hipStreamSynchronize(s);
+            return fail(ctx, FRI_ERCCL, "sharded commit: no progress in " + std::to_string((int)lim) +
+                                            " s (RCCL communicators aborted)");
+        }
+        std::this_thread::yield();
+    }
+}
 
 static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
     Transport& tp = ctx->tp;
@@ -1075,13 +1122,48 @@ extern "C" int fri_dist_attach_rccl(fri_ctx* ctx, int rank, int world, const uin
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     ncclUniqueId id;
     memcpy(id.internal, uid, 128);
-    ncclComm_t comm = nullptr, xcomm = nullptr;
-    FRI_NCCL(ctx, ncclCommInitRank(&comm, world, id, rank));
-    ncclResult_t r = ncclCommSplit(comm, 0, rank, &xcomm, nullptr);   // second comm for the exchange stream
-    if (r != ncclSuccess) {
-        ncclCommDestroy(comm);
-        return fail(ctx, FRI_ERCCL, std::string("ncclCommSplit: ") + ncclGetErrorString(r));
+    // communicator setup on a helper thread, waited for with the deadline; a
+    // thread still blocked in the rendezvous after it is abandoned (it frees
+    // what it creates if it ever finishes)
+    struct Setup {
+        std::mutex m;
+        std::condition_variable cv;
+        bool done = false, abandoned = false;
+        ncclComm_t comm = nullptr, xcomm = nullptr;
+        ncclResult_t r = ncclSuccess;
+        const char* what = "";
+    };
+    auto su = std::make_shared<Setup>();
+    const int dev = ctx->device;
+    std::thread([su, dev, world, id, rank]() {
+        (void)hipSetDevice(dev);
+        ncclComm_t c = nullptr, x = nullptr;
+        const char* what = "ncclCommInitRank";
+        ncclResult_t r = ncclCommInitRank(&c, world, id, rank);
+        if (r == ncclSuccess) {
+            what = "ncclCommSplit";
+            r = ncclCommSplit(c, 0, rank, &x, nullptr);      // second comm for the exchange stream
+            if (r != ncclSuccess) { ncclCommDestroy(c); c = nullptr; x = nullptr; }
+        }
+        std::lock_guard<std::mutex> g(su->m);
+        if (su->abandoned) {
+            if (x) ncclCommDestroy(x);
+            if (c) ncclCommDestroy(c);
+        } else {
+            su->comm = c; su->xcomm = x; su->r = r; su->what = what;
+        }
+        su->done = true;
+        su->cv.notify_all();
+    }).detach();
+    const double lim = rccl_timeout_s();
+    std::unique_lock<std::mutex> lk(su->m);
+    if (!su->cv.wait_for(lk, std::chrono::duration<double>(lim), [&] { return su->done; })) {
+        su->abandoned = true;
+        return fail(ctx, FRI_ERCCL, "RCCL rendezvous (rank " + std::to_string(rank) + " of " + std::to_string(world) +
+                                        ") did not complete in " + std::to_string((int)lim) + " s");
     }
+    if (su->r != ncclSuccess) return fail(ctx, FRI_ERCCL, std::string(su->what) + ": " + ncclGetErrorString(su->r));
+    ncclComm_t comm = su->comm, xcomm = su->xcomm;
     ctx->tp.comm = comm;
     ctx->tp.xcomm = xcomm;
     ctx->tp.rank = rank;
@@ -1135,7 +1217,7 @@ extern "C" int fri_dist_selftest(fri_ctx* ctx, size_t words_per_peer) {
     DistBuf& db = ctx->db;
     auto check = [&](const char* what, auto expect) -> int {
         FRI_HIP(ctx, hipMemcpyAsync(got.data(), db.recv, tot * 4, hipMemcpyDeviceToHost, s));
-        FRI_HIP(ctx, hipStreamSynchronize(s));
+        if (int rs = sync_sharded(ctx, s)) return rs;
         for (uint32_t p = 0; p < G; p++)
             for (size_t i = 0; i < W; i++)
                 if (got[p * W + i] != expect(p, (uint32_t)i))
@@ -1209,6 +1291,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     while ((1u << logG) < G) logG++;
     if (G == 1 || log_n < SHARD_MIN_LOG || log_n < logG + 12)
         return run_commit(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
+    if (!ctx->tp.host && !ctx->tp.comm) return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
     if (log_n > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n out of range for context");
     const size_t n = (size_t)1 << log_n;
     if (d > n) return fail(ctx, FRI_EDEGREE, "more coefficients than domain points (domain would be exhausted)");
@@ -1381,7 +1464,10 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     }
     FRI_HIP(ctx, hipGetLastError());
     FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
-    FRI_HIP(ctx, hipStreamSynchronize(s));
+    if ((rc = sync_sharded(ctx, s))) {
+        ctx->h_state->n_layers = 0;
+        return rc;
+    }
     if (ctx->profiling) spans_collect(ctx);
     DevState* h = ctx->h_state;
     if (h->status) {

@@ -98,3 +98,26 @@ def test_rccl_transport_selftest_world1():
         ctx.detach()
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_rccl_attach_times_out_without_peer(monkeypatch, oracle):
+    """A rendezvous that never completes (rank 0 of 2, rank 1 absent) ends in
+    FRI_ERCCL after FRI_RCCL_TIMEOUT_S instead of hanging, and the context
+    stays usable for 1-GPU commits.  (The abandoned setup thread stays blocked
+    in RCCL's bootstrap for the rest of the process: keep this test last among
+    the RCCL tests.)"""
+    import time
+    import fri_amd
+    monkeypatch.setenv("FRI_RCCL_TIMEOUT_S", "3")
+    ctx = fri_amd.Context(0, 20)
+    try:
+        t0 = time.monotonic()
+        with pytest.raises(fri_amd.FriError, match="rendezvous"):
+            ctx.attach_rccl(0, 2, fri_amd.Context.unique_id())
+        assert time.monotonic() - t0 < 60
+        coeffs = oracle.splitmix64_field(3, 128)
+        res = ctx.commit(coeffs, 10)
+        assert res.n_layers == 8
+    finally:
+        ctx.close()
