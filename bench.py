@@ -294,6 +294,13 @@ def main():
         pcie = {"ms_per_step": round(1000.0 * (time.perf_counter() - t0) / k, 4),
                 "what": f"fri_commit from a pageable host buffer of {d} u32 coefficients (H2D inside the call)"}
 
+    # Decommitment (fri_commit.rs:137-179) on the commit
+    # just made: one fri_decommit_query per query index gathers both values and
+    # both authentication paths of every layer.  Beside `value`, never it.
+    decommit = None
+    if world == 1 and mode == "single" and not args.no_extras:
+        decommit = _decommit_stage(fri_amd, ctx, res, log_n)
+
     # Trace side of the prover (BASELINE configs[3] trace length): 2^16 trace
     # -> iNTT -> coset LDE 2^19 -> Merkle commit, device-resident (reported
     # beside the metric, never `value`).
@@ -351,6 +358,7 @@ def main():
             "whole_commit": whole,
             "breakdown_ms_per_step": breakdown,
             "pcie_inclusive": pcie,
+            "decommit": decommit,
             "prover_trace_commit": trace_stage,
             "concurrent_commits": concurrent,
             "prover_fibsq": prover,
@@ -364,6 +372,46 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _decommit_stage(fri_amd, ctx, res, log_n, nq=64):
+    """fri_decommit_query through the C ABI (preallocated buffers) for nq
+    pseudo-random indices of the resident commit (transcript `res`); every
+    path of the first query is checked against the committed roots on the
+    host (hashlib)."""
+    import hashlib
+    import numpy as np
+    n_layers = ctx.commit_info()[2]
+    vals = np.empty(2 * n_layers, dtype=np.uint32)
+    total = sum(64 * (log_n - k) for k in range(n_layers))
+    buf = ctypes.create_string_buffer(total)
+    got = ctypes.c_size_t()
+    vptr = vals.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+    idx = [(0x9E3779B97F4A7C15 * (i + 1)) % (1 << log_n) for i in range(nq)]
+
+    def query(i):
+        ctx._check(ctx.lib.fri_decommit_query(ctx.h, i, vptr, vals.size, buf, total, ctypes.byref(got)))
+
+    query(idx[0])
+    ok, off, raw = True, 0, buf.raw
+    for k in range(n_layers):
+        depth, m = log_n - k, 1 << (log_n - k)
+        for v, j, path in ((int(vals[2 * k]), idx[0] % m, raw[off:off + 32 * depth]),
+                           (int(vals[2 * k + 1]), (idx[0] % m + m // 2) % m, raw[off + 32 * depth:off + 64 * depth])):
+            h = hashlib.sha256(v.to_bytes(8, "big")).digest()
+            for lvl in range(depth):
+                sib = path[32 * lvl:32 * lvl + 32]
+                h = hashlib.sha256(h + sib if j % 2 == 0 else sib + h).digest()
+                j //= 2
+            ok = ok and h == bytes(res.roots[k])
+        off += 64 * depth
+    t0 = time.perf_counter()
+    for i in idx:
+        query(i)
+    us = 1e6 * (time.perf_counter() - t0) / nq
+    return {"us_per_query": round(us, 1), "queries": nq, "layers": n_layers, "first_query_paths_verified": ok,
+            "what": "fri_decommit_query: both values and both authentication paths of every layer "
+                    "(one gather launch + one device-to-host copy per query)"}
 
 
 def _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C, steps):
