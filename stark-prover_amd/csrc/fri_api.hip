@@ -108,8 +108,8 @@ struct fri_ctx {
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
     uint64_t commit_gen = 0;        // bumped by every commit: read-backs of an older proof are refused
     uint32_t commit_log_n = 0;      // codeword log2 of the resident commit
-    uint32_t* dq_buf = nullptr;     // decommitment gather staging (64 KiB)
-    uint32_t* dq_host = nullptr;    // ... and its pinned host mirror (one DMA per query)
+    uint32_t* dq_host = nullptr;    // decommitment gather output: 64 KiB of coherent pinned host
+    uint32_t* dq_dev = nullptr;     // memory the gather kernel writes directly (its device address)
     uint32_t* trace_tree = nullptr; // Merkle tree of the last fri_trace_commit LDE
     uint32_t* trace_lde = nullptr;  // ... and the LDE itself (prover: composition, queries)
     size_t trace_tree_cap = 0;      // leaves they can hold
@@ -238,7 +238,6 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     hipFree(ctx->scratch_a); hipFree(ctx->scratch_b); hipFree(ctx->scratch_c);
     hipFree(ctx->pow_lo); hipFree(ctx->pow_hi);
     hipFree(ctx->d_state);
-    hipFree(ctx->dq_buf);
     if (ctx->dq_host) hipHostFree(ctx->dq_host);
     hipFree(ctx->trace_tree);
     hipFree(ctx->trace_lde);
@@ -796,10 +795,17 @@ extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint3
     return FRI_OK;
 }
 
-// 64 KiB device staging + pinned host mirror for the per-query gathers.
+// The gather kernel writes a query's values and paths (<= 64 KiB) straight
+// into coherent pinned host memory: no device-to-host copy per query (a copy
+// of that size took either ~25 or ~130 us per query, varying from process to
+// process; the zero-copy write does not go through the copy engines).
 static int dq_alloc(fri_ctx* ctx) {
-    if (!ctx->dq_buf) FRI_HIP(ctx, hipMalloc(&ctx->dq_buf, 65536));
-    if (!ctx->dq_host) FRI_HIP(ctx, hipHostMalloc(&ctx->dq_host, 65536, hipHostMallocDefault));
+    if (!ctx->dq_host) {
+        FRI_HIP(ctx, hipHostMalloc(&ctx->dq_host, 65536, hipHostMallocMapped | hipHostMallocCoherent));
+        void* d = nullptr;
+        FRI_HIP(ctx, hipHostGetDevicePointer(&d, ctx->dq_host, 0));
+        ctx->dq_dev = static_cast<uint32_t*>(d);
+    }
     return FRI_OK;
 }
 
@@ -829,9 +835,8 @@ extern "C" int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     int rc = dq_alloc(ctx);
     if (rc) return rc;
-    launch_decommit_gather(p.layers, p.trees, dp, ctx->dq_buf, ctx->stream);
+    launch_decommit_gather(p.layers, p.trees, dp, ctx->dq_dev, ctx->stream);
     FRI_HIP(ctx, hipGetLastError());
-    FRI_HIP(ctx, hipMemcpyAsync(ctx->dq_host, ctx->dq_buf, total, hipMemcpyDeviceToHost, ctx->stream));
     FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
     memcpy(values, ctx->dq_host, 2 * dp.n_layers * 4);
     memcpy(paths, ctx->dq_host + 2 * dp.n_layers, (size_t)words * 4);
@@ -931,9 +936,8 @@ extern "C" int fri_trace_decommit(fri_ctx* ctx, uint64_t index, uint64_t stride,
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     int rc = dq_alloc(ctx);
     if (rc) return rc;
-    launch_trace_gather(ctx->trace_lde, ctx->trace_tree, L, index, stride, count, ctx->dq_buf, ctx->stream);
+    launch_trace_gather(ctx->trace_lde, ctx->trace_tree, L, index, stride, count, ctx->dq_dev, ctx->stream);
     FRI_HIP(ctx, hipGetLastError());
-    FRI_HIP(ctx, hipMemcpyAsync(ctx->dq_host, ctx->dq_buf, (count + words) * 4, hipMemcpyDeviceToHost, ctx->stream));
     FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
     memcpy(values, ctx->dq_host, count * 4);
     memcpy(paths, ctx->dq_host + count, words * 4);
