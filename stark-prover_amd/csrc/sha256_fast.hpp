@@ -106,18 +106,6 @@ __device__ __forceinline__ void rounds_pad64(uint32_t st[8]) {
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-// Rounds with a K+W table in memory (uniform -> scalar loads).
-__device__ __forceinline__ void rounds_kwtab(uint32_t st[8], const uint32_t* kw) {
-    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
-    for (int t = 0; t < 64; t++) {
-        uint32_t t1 = h + kw[t] + S1(e) + chf(e, f, g);
-        uint32_t t2 = S0(a) + majf(a, b, c);
-        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
-    }
-    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
-}
-
 // ---- compact forms for latency-bound code (executed once per launch, so
 // I-cache footprint matters more than the last few percent of issue rate):
 // 16 rounds unrolled, looped 4x; K and padding schedules via scalar loads.
