@@ -596,9 +596,9 @@ static void enqueue_commit(fri_ctx* ctx) {
     span_end(ctx, sp);
     for (int k = 0; k <= p.rmax; k++) {
         const uint32_t L = log_n - (uint32_t)k;
-        if (L <= TOP_LOG) {
+        if (L <= TAIL_LOG) {
             // the remaining small layers: one single-workgroup launch
-            LayerTask ts[TOP_LOG + 1];
+            LayerTask ts[TAIL_LOG + 1];
             uint32_t nt = 0;
             for (int kk = k; kk <= p.rmax; kk++) ts[nt++] = commit_task(ctx, kk);
             size_t spk = span_begin(ctx, k == 0 ? "layer0" : "layers", 0);
@@ -1454,8 +1454,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
             FRI_HIP(ctx, hipMemcpyAsync(p.layers + p.layer_off[k] + (size_t)block_of[r] * B, db.gath + (size_t)r * B,
                                         B * 4, hipMemcpyDeviceToDevice, s));
         for (int kk = k + 1; kk <= p.rmax; kk++) {
-            if (log_n - (uint32_t)kk <= TOP_LOG) {       // small layers: one launch
-                LayerTask ts[TOP_LOG + 1];
+            if (log_n - (uint32_t)kk <= TAIL_LOG) {      // small layers: one launch
+                LayerTask ts[TAIL_LOG + 1];
                 uint32_t nt = 0;
                 for (int k2 = kk; k2 <= p.rmax; k2++) ts[nt++] = commit_task(ctx, k2);
                 launch_tail(ts, nt, s);

@@ -10,6 +10,10 @@ namespace fri {
 
 constexpr int MAXR = 32;            // == FRI_MAX_ROUNDS
 constexpr uint32_t TOP_LOG = 9;         // single-workgroup tree top: <= 512 inputs
+#ifndef FRI_TAIL_LOG
+#define FRI_TAIL_LOG 9
+#endif
+constexpr uint32_t TAIL_LOG = FRI_TAIL_LOG;   // layers of <= 2^TAIL_LOG elements run in the fused tail
 constexpr uint32_t POW_LO_LOG = 12;     // two-level power tables s^j = lo[j&4095]*hi[j>>12]
 
 // Device-resident commit state (one per context).  Every per-round kernel
@@ -102,8 +106,8 @@ struct LayerTask {
     int gidx;                  //   layers): skip when !gst->active[gidx]
 };
 void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end = nullptr);
-// Layers ts[0..n) (consecutive, 2^L <= 2^TOP_LOG elements, commit mode) in
-// one single-workgroup launch (k_tree_tail), n <= TOP_LOG + 1.
+// Layers ts[0..n) (consecutive, 2^L <= 2^TAIL_LOG elements, commit mode) in
+// one single-workgroup launch (k_tree_tail), n <= TAIL_LOG + 1.
 void launch_tail(const LayerTask* ts, uint32_t n, hipStream_t s);
 // Coefficient task of layer t.k alone (grid G): k == 0 scans the input for
 // deg_0, k >= 1 folds poly_{k-1} -> poly_k; maxima into t.wgmax[3*G].

@@ -671,7 +671,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
 }
 
 // ------------------------------------------------------------- tail ----
-// The last layers of a commit (2^L <= 2^TOP_LOG elements each) in ONE
+// The last layers of a commit (2^L <= 2^TAIL_LOG elements each) in ONE
 // workgroup and ONE launch: per layer the body of k_tree_top<true, *, true>
 // (fold, leaves, coefficient fold, degree, tree levels, channel step), with
 // the layer values, the coefficients, beta, the degree and the gate handed to
@@ -679,7 +679,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
 // round trip of the folded values and coefficients, and the cold first level
 // of a fresh workgroup.  The channel state stays in wave 7's registers.
 struct TailTask {
-    LayerTask t[TOP_LOG + 1];   // consecutive layers k0 .. k0 + n - 1 (commit mode)
+    LayerTask t[TAIL_LOG + 1];  // consecutive layers k0 .. k0 + n - 1 (commit mode)
     uint32_t n;
 };
 
@@ -687,9 +687,10 @@ template <bool FOLD0>
 __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
     const LayerTask& t0 = tt.t[0];
     if (gated_off(t0)) return;
-    __shared__ uint4 lds[2 * 512 + 2 * 256];
-    __shared__ uint32_t vals[2][512];          // this / previous layer's values
-    __shared__ uint32_t coefs[2][512];         // this / previous round's polynomial
+    constexpr uint32_t NMAX = 1u << TAIL_LOG;
+    __shared__ uint4 lds[2 * NMAX + NMAX];
+    __shared__ uint32_t vals[2][NMAX];         // this / previous layer's values
+    __shared__ uint32_t coefs[2][NMAX];        // this / previous round's polynomial
     __shared__ int32_t red[24];
     __shared__ uint32_t s_beta_m, s_active;
     __shared__ int32_t s_deg;
@@ -719,7 +720,7 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
         uint32_t* cur_c = coefs[li & 1];
         const uint32_t* prev_c = coefs[(li & 1) ^ 1];
         uint4* A = lds;
-        uint4* B = lds + 2 * 512;
+        uint4* B = lds + 2 * NMAX;
         uint32_t* tr = t.tree;
         // ---- fold + leaves (spare lanes of wave 0 recompute leaf i mod N) ----
         for (uint32_t i = tid; i < max(N, 64u); i += blockDim.x) {
