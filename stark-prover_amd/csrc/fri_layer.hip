@@ -149,6 +149,9 @@ __device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32
     }
 }
 
+#ifndef FRI_QUAD_LEAVES_FIRST
+#define FRI_QUAD_LEAVES_FIRST 1
+#endif
 // Four consecutive level-l digests (or leaves) per thread -> level l+2 node.
 // lv0/lv1 are this layer's level l+0 / l+1 arrays (lv0 written only for
 // leaves: it is the input otherwise).
@@ -156,6 +159,21 @@ template <bool LEAVES>
 __device__ __forceinline__ void quad(const uint4& vals, const uint32_t* in0, uint32_t* lv0, uint32_t* lv1,
                                      size_t q /*quad index*/, Dg& out) {
     Dg a, b, n0, n1;
+#if FRI_QUAD_LEAVES_FIRST
+    if (LEAVES) {
+        // all four leaves first: the thread's 128 contiguous level-l bytes are
+        // written close together in time, and so are its two level-(l+1) digests
+        Dg c, d;
+        hleaf(vals.x, a); hleaf(vals.y, b); dg_store(lv0 + 8 * (4 * q), a); dg_store(lv0 + 8 * (4 * q + 1), b);
+        hleaf(vals.z, c); hleaf(vals.w, d); dg_store(lv0 + 8 * (4 * q + 2), c); dg_store(lv0 + 8 * (4 * q + 3), d);
+        hnode(a, b, n0);
+        hnode(c, d, n1);
+        dg_store(lv1 + 8 * (2 * q), n0);
+        dg_store(lv1 + 8 * (2 * q + 1), n1);
+        hnode(n0, n1, out);
+        return;
+    }
+#endif
     if (LEAVES) { hleaf(vals.x, a); hleaf(vals.y, b); dg_store(lv0 + 8 * (4 * q), a); dg_store(lv0 + 8 * (4 * q + 1), b); }
     else { dg_load(in0 + 8 * (4 * q), a); dg_load(in0 + 8 * (4 * q + 1), b); }
     hnode(a, b, n0);
