@@ -6,7 +6,7 @@
 //   k_layer_leaf  (2^(L-10) workgroups, L >= 11)
 //       fold of layer k-1 with beta_{k-1}      (src/fri/fri_commit.rs:53-65)
 //       leaf hashes SHA256(u64_be(v))           (src/merkle/mod.rs:14-15)
-//       tree levels 1..4 (1024 leaves -> 64 nodes per workgroup)
+//       tree levels 1..4 (2048 leaves -> 128 nodes per workgroup)
 //       a slice of the coefficient fold of round k-1 (fri_commit.rs:32-50)
 //       with per-workgroup maxima (no hot atomics) for the exact degree
 //   k_tree_mid    (levels l -> l+4, 1024 nodes in / 64 out per workgroup)
@@ -220,7 +220,7 @@ template <bool FOLD, bool COMMIT, uint32_t TPB>
 __global__ __launch_bounds__(TPB) void k_layer_leaf(LayerTask t) {
     if (gated_off(t)) return;
     __shared__ uint4 lds[3 * TPB];
-    __shared__ int32_t red[12];
+    __shared__ int32_t red[3 * (TPB / 64)];
     const uint32_t L = t.L;
     const size_t q = (size_t)blockIdx.x * TPB + threadIdx.x;   // quad index: leaves 4q..4q+3
     uint4 v;
@@ -879,7 +879,7 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
 // ------------------------------------------------------------ launcher ----
 // Layer schedule (levels are consumed 4 at a time):
 //   L <= 9 : one k_tree_top from the leaves.
-//   L >= 19: k_layer_leaf (1024 leaves/WG -> 64);  11..18: k_layer_leaf_wide (256 -> 16)
+//   L >= 19: k_layer_leaf (2048 leaves/WG -> 128);  11..18: k_layer_leaf_wide (256 -> 16)
 //   then k_tree_mid<1024> while the level has >= 2^18 nodes, k_tree_mid<256>
 //   while it has > 512, and k_tree_top on the last <= 512 nodes.
 static LayerTask with_gate(const LayerTask& in) {
@@ -892,7 +892,7 @@ static LayerTask with_gate(const LayerTask& in) {
 #define MID8 1               // k_tree_mid8 for the narrow levels of large layers
 #endif
 #ifndef QUAD_TPB
-#define QUAD_TPB 256         // quad leaf kernel: threads per WG (1024 leaves per WG)
+#define QUAD_TPB 512         // quad leaf kernel: threads per WG (2048 leaves per WG; A/B: 512 beats 256 by ~0.5-1%, 128 and 1024 slower)
 #endif
 #ifndef QUAD_MIN_LOG
 #define QUAD_MIN_LOG 19      // smaller layers: one leaf per lane (A/B: 19 beats 20 and 21)
