@@ -162,10 +162,12 @@ __device__ __forceinline__ void quad(const uint4& vals, const uint32_t* in0, uin
 #if FRI_QUAD_LEAVES_FIRST
     if (LEAVES) {
         // all four leaves first: the thread's 128 contiguous level-l bytes are
-        // written close together in time, and so are its two level-(l+1) digests
+        // written together (no partly written line waits in L2 for its other
+        // half), and so are its two level-(l+1) digests
         Dg c, d;
-        hleaf(vals.x, a); hleaf(vals.y, b); dg_store(lv0 + 8 * (4 * q), a); dg_store(lv0 + 8 * (4 * q + 1), b);
-        hleaf(vals.z, c); hleaf(vals.w, d); dg_store(lv0 + 8 * (4 * q + 2), c); dg_store(lv0 + 8 * (4 * q + 3), d);
+        hleaf(vals.x, a); hleaf(vals.y, b); hleaf(vals.z, c); hleaf(vals.w, d);
+        dg_store(lv0 + 8 * (4 * q), a); dg_store(lv0 + 8 * (4 * q + 1), b);
+        dg_store(lv0 + 8 * (4 * q + 2), c); dg_store(lv0 + 8 * (4 * q + 3), d);
         hnode(a, b, n0);
         hnode(c, d, n1);
         dg_store(lv1 + 8 * (2 * q), n0);
