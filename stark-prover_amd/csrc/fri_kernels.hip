@@ -44,6 +44,9 @@ __device__ __forceinline__ uint32_t pow2lvl(const uint32_t* lo, const uint32_t* 
 #endif
 __device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4) + (NTT_PAD10 ? (x >> 10) << 1 : 0u); }
 
+#ifndef NTT_VEC
+#define NTT_VEC 1            // 16-byte load/store phases where the tile allows (launch_pass)
+#endif
 #ifndef NTT_TPB
 #define NTT_TPB 512          // threads per NTT tile (16 elements each; 512: 128-byte row runs)
 #endif
@@ -52,7 +55,12 @@ __device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4) 
 // bit-reversal gather every row q with q mod 2^Z != 0 is zero and DIT stages
 // 0..Z-1 only copy a row into its zero partners (u + w*0 = u - w*0 = u):
 // they become register copies (an LDE of blowup 8 skips 3 of its log_n stages).
-template <int A, int B, bool FIRST, int TPB, int Z = 0>
+// VEC: full tiles of 32 contiguous columns (NS = 8, n >= TILE, 16-byte
+// aligned buffers, s0 >= 2): the load and store phases move 4 consecutive
+// words per lane as one 16-byte access, all four of a lane's accesses issued
+// before the first LDS write (or HBM store), instead of 16 4-byte accesses
+// issued four at a time.
+template <int A, int B, bool FIRST, int TPB, int Z = 0, bool VEC = false>
 __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d, uint32_t* dst,
                                                   uint32_t log_n, uint32_t s0, const uint32_t* __restrict__ tw,
                                                   const uint32_t* __restrict__ pre_lo, const uint32_t* __restrict__ pre_hi,
@@ -75,6 +83,45 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
         return ((col >> s0) << (s0 + NS)) + ((size_t)q << s0) + (col & lomask);
     };
     // ---- load (contiguous runs across the tile's columns) -----------------
+    if (VEC) {
+        static_assert(!VEC || C % 4 == 0, "vector phases need whole 4-column groups");
+        constexpr uint32_t VPR = C / 4;          // 16-byte vectors per tile row
+        uint4 v4[4];
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++) {
+            const uint32_t y = r * TPB + tid;
+            const uint32_t c = (y % VPR) * 4, q = y / VPR;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (FIRST) {
+                const size_t si = ((size_t)(__brev(q) >> (32 - NS)) << cbits) + col0 + c;
+                if (si + 3 < d) {
+                    v = *reinterpret_cast<const uint4*>(src + si);
+                } else if (si < d) {   // the vector straddling d: zeros beyond it
+                    v.x = src[si];
+                    if (si + 1 < d) v.y = src[si + 1];
+                    if (si + 2 < d) v.z = src[si + 2];
+                }
+                if (pre_lo && si < d) {
+                    v.x = pow2lvl(pre_lo, pre_hi, si, v.x);
+                    v.y = pow2lvl(pre_lo, pre_hi, si + 1, v.y);
+                    v.z = pow2lvl(pre_lo, pre_hi, si + 2, v.z);
+                    v.w = pow2lvl(pre_lo, pre_hi, si + 3, v.w);
+                }
+            } else {
+                v = *reinterpret_cast<const uint4*>(src + gidx(c, q));
+            }
+            v4[r] = v;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++) {
+            const uint32_t y = r * TPB + tid;
+            const uint32_t c = (y % VPR) * 4, q = y / VPR;
+            lds[ntt_laddr(c * P + q)] = v4[r].x;
+            lds[ntt_laddr((c + 1) * P + q)] = v4[r].y;
+            lds[ntt_laddr((c + 2) * P + q)] = v4[r].z;
+            lds[ntt_laddr((c + 3) * P + q)] = v4[r].w;
+        }
+    } else
 #pragma unroll 4
     for (uint32_t r = 0; r < 16; r++) {
         const uint32_t y = r * TPB + tid;
@@ -177,6 +224,23 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
     }
     __syncthreads();
     // ---- store (contiguous runs) ------------------------------------------
+    if (VEC) {
+#pragma unroll
+        for (uint32_t rr = 0; rr < 4; rr++) {
+            const uint32_t y = rr * TPB + tid;
+            uint32_t c, q, w[4];     // first element of the vector: 4 rows (FIRST) or 4 columns
+            if (FIRST) { c = y / (P / 4); q = (y % (P / 4)) * 4; } else { c = (y % (C / 4)) * 4; q = y / (C / 4); }
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) w[j] = lds[ntt_laddr(FIRST ? c * P + q + j : (c + j) * P + q)];
+            const size_t g = gidx(c, q);
+            if (post_lo) {
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++) w[j] = pow2lvl(post_lo, post_hi, g + j, w[j]);
+            }
+            *reinterpret_cast<uint4*>(dst + g) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        return;
+    }
 #pragma unroll 4
     for (uint32_t rr = 0; rr < 16; rr++) {
         const uint32_t y = rr * TPB + tid;
@@ -214,6 +278,14 @@ static void launch_pass(uint32_t ns, const uint32_t* src, size_t d, uint32_t* ds
         hipLaunchKernelGGL((k_ntt_pass<AV, BV, FIRST, TPB, (Z < AV ? Z : AV)>), dim3(blocks), dim3(TPB), 0, s, src, d, \
                            dst, log_n, s0, p.tw, plo, phi, qlo, qhi);                                           \
         break;
+    // vector load/store phases: whole tiles of 32 contiguous columns, 16-byte aligned buffers
+    const bool vec = NTT_VEC && ns == 8 && n >= 16u * TPB && (FIRST || s0 >= 2) &&
+                     ((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0;
+    if (vec) {
+        hipLaunchKernelGGL((k_ntt_pass<4, 4, FIRST, TPB, (Z < 4 ? Z : 4), true>), dim3(blocks), dim3(TPB), 0, s, src,
+                           d, dst, log_n, s0, p.tw, plo, phi, qlo, qhi);
+        return;
+    }
     switch (ns) {
         NTT_CASE(1, 1, 0) NTT_CASE(2, 2, 0) NTT_CASE(3, 3, 0) NTT_CASE(4, 4, 0)
         NTT_CASE(5, 4, 1) NTT_CASE(6, 4, 2) NTT_CASE(7, 4, 3) NTT_CASE(8, 4, 4)
