@@ -47,6 +47,9 @@ __device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4) 
 #ifndef NTT_VEC
 #define NTT_VEC 1            // 16-byte load/store phases where the tile allows (launch_pass)
 #endif
+#ifndef NTT_TWS
+#define NTT_TWS 1            // small twiddle table staged in LDS (phase B reads it per lane)
+#endif
 #ifndef NTT_TPB
 #define NTT_TPB 512          // threads per NTT tile (16 elements each; 512: 128-byte row runs)
 #endif
@@ -69,7 +72,9 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
     // tile: 16 elements per thread; C columns (C consecutive words per row)
     constexpr uint32_t NS = A + B, P = 1u << NS, TILE = 16u * TPB, C = TILE / P;
     __shared__ uint32_t lds[TILE + TILE / 16 + 2 * (TILE >> 10)];
+    __shared__ uint32_t tws[NTT_TWS ? P : 1];   // the pass's small twiddle table tw[0 .. 2^NS), read per lane in phase B
     const uint32_t tid = threadIdx.x;
+    if (NTT_TWS && tid < P) tws[tid] = tw[tid];
     const size_t ncols = ((size_t)1 << log_n) >> NS;
     const size_t col0 = (size_t)blockIdx.x * C;
     const size_t lomask = ((size_t)1 << s0) - 1;
@@ -157,7 +162,8 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
         for (int t = (int)NS - 2; t >= 0; t--) wl[t] = mmul(wl[t + 1], wl[t + 1]);
     }
     auto twid = [&](int t, uint32_t q0) -> uint32_t {
-        const uint32_t w = tw[(1u << t) + (q0 & ((1u << t) - 1))];
+        const uint32_t j = q0 & ((1u << t) - 1);
+        const uint32_t w = NTT_TWS ? tws[(1u << t) + j] : tw[(1u << t) + j];
         return FIRST ? w : mmul(w, wl[t]);
     };
     // ---- phase A: stages 0..A-1 on 16 consecutive elements ----------------
@@ -174,10 +180,13 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
             for (int e = 0; e < 16; e++) {
                 if (e & (1 << t)) continue;
                 const uint32_t q0 = (x0 + e) & (P - 1);
-                // first pass: row q0 = x0 + e with x0 a multiple of 16, so the
-                // twiddle w_{2^(t+1)}^(e mod 2^t) is 1 at e mod 2^t == 0
-                const bool one = FIRST && (e & ((1 << t) - 1)) == 0;
-                const uint32_t u = r[e], v = one ? r[e + (1 << t)] : mmul(r[e + (1 << t)], twid(t, q0));
+                // row q0 = x0 + e with x0 a multiple of 16, so the small-table
+                // twiddle w_{2^(t+1)}^(e mod 2^t) is 1 at e mod 2^t == 0: no
+                // multiply in the first pass, the column factor alone in later ones
+                const bool j0 = (e & ((1 << t) - 1)) == 0;
+                const uint32_t u = r[e];
+                const uint32_t v = (FIRST && j0) ? r[e + (1 << t)]
+                                                 : mmul(r[e + (1 << t)], (!FIRST && j0) ? wl[t < NS ? t : 0] : twid(t, q0));
                 r[e] = add(u, v);
                 r[e + (1 << t)] = sub(u, v);
             }
