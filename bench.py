@@ -261,14 +261,22 @@ def main():
                         "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"], "frac": top["frac"],
                         "traffic": None, "avg_launch_ms": round(avg_ms, 4), "launches": launches,
                         "hbm": hbm, "valu": valu}
-            # the HBM-bound kernel of the path: the coset-LDE NTT (algorithmic
-            # bytes 4d read + 4n written per commit)
+            # the HBM-shaped kernel of the path: the coset-LDE NTT (algorithmic
+            # bytes 4d read + 4n written per commit).  Its passes move more:
+            # the first reads 4d and writes 4n, every later pass reads and
+            # writes 4n (8-stage passes); PMC puts them at about
+            # 0.85 VALU instructions per quad-cycle per SIMD.
             lms, ll, lbytes = ctx.profile("lde")
             if ll:
-                lde_gbs = (lbytes / ll) / (lms / ll * 1e-3) / 1e9
-                roofline["lde_ntt"] = {"bound": "hbm", "achieved": round(lde_gbs, 2), "peak": HBM_PEAK_GBS,
-                                       "unit": "GB/s", "frac": round(lde_gbs / HBM_PEAK_GBS, 4),
-                                       "bytes_per_launch": lbytes / ll, "avg_launch_ms": round(lms / ll, 4)}
+                lde_s = lms / ll * 1e-3
+                lde_gbs = (lbytes / ll) / lde_s / 1e9
+                npass = (log_n + 7) // 8 if mode != "sharded" else None
+                pass_bytes = (4 * d + 4 * n + 8 * n * (npass - 1)) if npass else None
+                roofline["lde_ntt"] = {"bound": "hbm", "limiter": "valu issue (PMC)", "achieved": round(lde_gbs, 2),
+                                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(lde_gbs / HBM_PEAK_GBS, 4),
+                                       "bytes_per_launch": lbytes / ll, "avg_launch_ms": round(lms / ll, 4),
+                                       "passes": npass, "pass_bytes_per_launch": pass_bytes,
+                                       "pass_GBs": round(pass_bytes / lde_s / 1e9, 2) if pass_bytes else None}
         breakdown = {}
         for cls in ("lde", "alltoall", "merkle_layer0_leaf", "layer0", "layers", "gather"):
             cms, cl, _ = ctx.profile(cls)
