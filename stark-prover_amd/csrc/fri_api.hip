@@ -131,9 +131,16 @@ static int fail(fri_ctx* ctx, int code, const std::string& msg) {
     return code;
 }
 
+// Every value < p.  A branch-free max over 64 KiB blocks (the compiler
+// vectorises it), with the early exit per block: the per-element early-exit
+// loop cost about 1 ms per 2^21 coefficients of fri_commit's host input.
 static bool check_canonical(const uint32_t* v, size_t n) {
-    for (size_t i = 0; i < n; i++)
-        if (v[i] >= P) return false;
+    for (size_t i = 0; i < n; i += 16384) {
+        const size_t e = n - i < 16384 ? n : i + 16384;
+        uint32_t mx = 0;
+        for (size_t j = i; j < e; j++) mx = v[j] > mx ? v[j] : mx;
+        if (mx >= P) return false;
+    }
     return true;
 }
 

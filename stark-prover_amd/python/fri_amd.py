@@ -132,6 +132,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 
 
 def _u32(a) -> np.ndarray:
+    if isinstance(a, np.ndarray) and a.dtype == np.uint32:
+        # no widening copy: every library entry point checks canonicity itself
+        # (FRI_EINVAL, raised by _check); the uint64 round trip below cost
+        # about 1.5 ms per 2^21 coefficients
+        return np.ascontiguousarray(a)
     arr = np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
     if arr.size and int(arr.max()) >= P:
         raise FriError(FRI_EINVAL, "field element not canonical (>= p)")
