@@ -49,7 +49,12 @@ def test_batch_inverse_edges(ctx):
 # --------------------------------------------------------------- poly: LDE --
 @pytest.mark.parametrize("log_n,d", [(1, 1), (1, 2), (3, 1), (4, 2), (6, 8), (10, 128), (12, 512),
                                      (13, 1024), (14, 2048), (16, 8192), (17, 100), (20, 1 << 17),
-                                     (22, 1 << 19), (12, 4096)])
+                                     (22, 1 << 19), (12, 4096),
+                                     # 16-byte load/store phases (k_ntt_pass VEC): full tiles from
+                                     # n = 2^13; a first pass of 8 stages whose last loaded vector
+                                     # straddles d (d mod 4 = 1, 2, 3), blowup 1, n = one tile
+                                     (16, 8189), (16, 8190), (16, 8191), (16, 1 << 16), (13, 8191),
+                                     (13, 1 << 13), (24, (1 << 21) - 3)])
 def test_lde_matches_oracle(ctx, corc, log_n, d):
     c = rng_field(log_n * 100 + d, d)
     got = ctx.lde(c, log_n, 5)
