@@ -677,16 +677,19 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
     hipStream_t s = ctx->stream;
     ctx->sharded_layers = 0;
     init_state(ctx, chan_in, flags, forced_betas);
-    FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
     if (host_coeffs && d)
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
     else if (dev_coeffs && dev_coeffs != p.d_in && d)
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, s));
     const bool use_graph = !(flags & FRI_FLAG_NO_GRAPH) && !ctx->profiling;
     if (use_graph) {
+        // the DevState copies in (from the pinned h_state just written) and out
+        // are nodes of the graph: no host API call between the commits' kernels
         if (!p.exec) {
             FRI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
             enqueue_commit(ctx);
+            FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
             hipGraph_t g = nullptr;
             FRI_HIP(ctx, hipStreamEndCapture(s, &g));
             p.graph = g;
@@ -694,10 +697,11 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
         }
         FRI_HIP(ctx, hipGraphLaunch(p.exec, s));
     } else {
+        FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
         enqueue_commit(ctx);
         FRI_HIP(ctx, hipGetLastError());
+        FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
     }
-    FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
     FRI_HIP(ctx, hipStreamSynchronize(s));
     if (ctx->profiling) spans_collect(ctx);
     DevState* h = ctx->h_state;
