@@ -21,12 +21,15 @@
  *
  * Parity status: field / polynomial / interpolation are pinned by the
  * reference's 60 unit-test KATs.  SHA-256 is pinned by FIPS 180-4 vectors and
- * Python hashlib.  rs_merkle tree shape, channel string encoding and U256
- * reduction are restated from the pinned third-party crates' published
- * behaviour (rs_merkle 1.4.2, sha256 1.5.0, alloy-primitives 0.8.21) — those
- * crates are not vendored and the reference has no tests for them:
- * PARITY UNPINNED for merkle/channel/fri beyond this repo's frozen spec
- * (SURVEY.md §8 "Frozen spec") and committed golden vectors.
+ * Python hashlib.  The rs_merkle 1.4.2 tree shape (pairing, odd-node
+ * promotion) is pinned by rs_merkle's documented example root over the
+ * SHA-256 leaves of "a".."f" (tests/test_oracle_kats.py, via the Python twin,
+ * which this file matches for every tree size 1..40).  The channel string
+ * encoding and U256 reduction are restated from the reference's channel.rs and
+ * the pinned crates' published behaviour (sha256 1.5.0, alloy-primitives
+ * 0.8.21) — not vendored, and the reference has no tests for them: PARITY
+ * UNPINNED for channel/fri beyond this repo's frozen spec (SURVEY.md §8
+ * "Frozen spec") and committed golden vectors.
  */
 #include <stdint.h>
 #include <stdlib.h>

@@ -10,7 +10,8 @@ C oracle's), so C-oracle == Python-twin checks pin the C SHA-256, the Merkle
 tree shape and the channel encoding against a second implementation.
 
 Parity status (see DESIGN.md "Oracle"): field / polynomial / interpolation
-semantics are pinned by the reference's unit-test KATs; rs_merkle tree shape,
+semantics are pinned by the reference's unit-test KATs; the rs_merkle tree
+shape (pairing and odd-node promotion) by rs_merkle's documented example root;
 channel hex/U256 encoding and the FRI transcript are restated from the frozen
 spec — PARITY UNPINNED beyond this repo's golden vectors.
 """
@@ -215,7 +216,14 @@ def merkle_levels(values: Sequence[int]) -> List[List[bytes]]:
     parent = SHA256(l || r); a lone right-most node is promoted."""
     if not values:
         raise ValueError("empty tree has no root")      # mod.rs:25 unwrap panics
-    lvl = [hashlib.sha256(fe_to_bytes(v)).digest() for v in values]
+    return merkle_levels_from_leaves([hashlib.sha256(fe_to_bytes(v)).digest() for v in values])
+
+
+def merkle_levels_from_leaves(lvl: List[bytes]) -> List[List[bytes]]:
+    """rs_merkle 1.4.2 ``MerkleTree::<Sha256>::from_leaves`` over leaf digests
+    (mod.rs:15-19): parent = SHA256(l || r), a lone right-most node promoted
+    unchanged.  Pinned by rs_merkle's own documented example (the root of the
+    SHA-256 leaves of "a".."f", tests/test_oracle_kats.py)."""
     levels = [lvl]
     while len(lvl) > 1:
         nxt = []

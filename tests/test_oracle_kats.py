@@ -307,3 +307,31 @@ def test_interpolation_roundtrip_random(F, oracle):                         # :2
         xs = rng.sample(range(1, 10**6), deg + 1)
         ys = [F.evaluate(coeffs, x, p) for x in xs]
         assert F.interpolate(xs, ys, p) == coeffs
+
+
+# ------------------------------------- third party: rs_merkle 1.4.2 (Cargo.lock:3456-3462)
+def test_rs_merkle_documented_root(oracle):
+    """rs_merkle's own documented example (crate README / `MerkleTree` docs):
+    `MerkleTree::<Sha256>::from_leaves` over the SHA-256 digests of the
+    strings "a".."f" has root_hex 1f7379...4da2.  Six leaves take the odd-node
+    path on level 1 (three nodes, the last promoted unchanged), so this pins
+    both the pairing and the promotion that src/merkle/mod.rs:15-25 inherits."""
+    import hashlib
+    leaves = [hashlib.sha256(s.encode()).digest() for s in "abcdef"]
+    levels = oracle.merkle_levels_from_leaves(leaves)
+    assert [len(lv) for lv in levels] == [6, 3, 2, 1]
+    assert levels[1][2] == hashlib.sha256(leaves[4] + leaves[5]).digest()
+    assert levels[2][1] == levels[1][2]                       # promoted, not re-hashed
+    assert levels[-1][0].hex() == "1f7379539707bcaea00564168d1d4d626b09b73f8a2a365234c62d763f854da2"
+
+
+def test_rs_merkle_shape_c_oracle_matches_twin(oracle, corc):
+    """The C oracle's tree (orc_merkle_build over field values) has the twin's
+    shape for every size 1..40, so the documented root above pins it too."""
+    import ctypes as ct
+    for n in range(1, 41):
+        vals = [(7919 * i + 3) % 3221225473 for i in range(n)]
+        cnt = corc.orc_merkle_nodes_count(n)
+        nodes = ct.create_string_buffer(32 * cnt)
+        corc.orc_merkle_build(c_arr(vals), n, nodes)
+        assert nodes.raw[32 * (cnt - 1): 32 * cnt].hex() == oracle.merkle_root_hex(vals)
