@@ -335,3 +335,26 @@ def test_rs_merkle_shape_c_oracle_matches_twin(oracle, corc):
         nodes = ct.create_string_buffer(32 * cnt)
         corc.orc_merkle_build(c_arr(vals), n, nodes)
         assert nodes.raw[32 * (cnt - 1): 32 * cnt].hex() == oracle.merkle_root_hex(vals)
+
+
+# ------------------- third party: sha256 1.5.0 and const-hex 1.14.0 (channel.rs:35-84)
+def test_channel_sha256_crate_documented_digest(oracle):
+    """sha256 1.5.0's documented example: digest("hello") is the lowercase hex
+    2cf24d…9824.  Channel::send sets state = sha256::digest(state ‖ hex(msg))
+    (channel.rs:35-40), so a state of "hello" and an empty message must give
+    exactly that string."""
+    ch = oracle.Channel(state="hello")
+    ch.send(b"")
+    assert ch.state == "2cf24dba5fb0a30e26e83b2ac5b9e29e1b161e5c1fa7425e73043362938b9824"
+
+
+def test_channel_hex_crate_documented_encoding(oracle):
+    """hex::encode (const-hex, the hex-crate API alloy re-exports; channel.rs:6,38)
+    is documented as hex::encode("Hello world!") == "48656c6c6f20776f726c6421":
+    lowercase, no prefix.  send hashes exactly that text after the old state."""
+    import hashlib
+    ch = oracle.Channel()
+    ch.send(b"Hello world!")
+    assert ch.state == hashlib.sha256(b"48656c6c6f20776f726c6421").hexdigest()
+    beta = oracle.Channel(state=ch.state).receive_random_field_element()
+    assert beta == int(ch.state, 16) % 3221225473           # U256::from_str_radix(state, 16) % p, min = 0
