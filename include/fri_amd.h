@@ -108,6 +108,18 @@ int fri_lde(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n,
 int fri_interpolate(fri_ctx* ctx, const uint32_t* ys, uint32_t log_n, uint32_t offset,
                     uint32_t* coeffs_out, size_t* len_out);
 
+/* Interpolation through n arbitrary points: Polynomial::interpolate(xs, ys)
+ * (src/polynomial/ops.rs:239-241 -> interpolate_lagrange_polynomials,
+ * interpolation.rs:121-152) for point sets that are not a coset.  Same
+ * result as the reference's Lagrange sum, duplicates included (their basis
+ * polynomials vanish through inverse(0) = 0, element.rs:54-57).  O(n^2) on
+ * the device: weights w_j = 1/prod_{i!=j}(x_j - x_i), then f at the 2^k-th
+ * roots of unity (2^k >= n) as the polynomial sum_j y_j w_j prod_{i!=j}(x - x_i)
+ * without any division, then an iNTT.  n <= 2^17 and n <= 2^log_n_max.
+ * coeffs_out holds n entries; *len_out = trimmed length. */
+int fri_interpolate_points(fri_ctx* ctx, const uint32_t* xs, const uint32_t* ys, size_t n,
+                           uint32_t* coeffs_out, size_t* len_out);
+
 /* Evaluation of P (d coefficients) at `count` arbitrary points
  * (src/polynomial/ops.rs:76-83, Horner semantics). */
 int fri_evaluate(fri_ctx* ctx, const uint32_t* coeffs, size_t d, const uint32_t* xs,

@@ -328,6 +328,44 @@ extern "C" int fri_interpolate(fri_ctx* ctx, const uint32_t* ys, uint32_t log_n,
     return FRI_OK;
 }
 
+// interpolate_lagrange_polynomials (interpolation.rs:121-152) on arbitrary
+// points: weights, c_j = y_j w_j, f on the 2^k-th roots of unity, iNTT
+// (fri_kernels.hip "arbitrary-point interpolate").
+extern "C" int fri_interpolate_points(fri_ctx* ctx, const uint32_t* xs, const uint32_t* ys, size_t n,
+                                      uint32_t* coeffs_out, size_t* len_out) {
+    if (!ctx || !len_out || (n && (!xs || !ys || !coeffs_out))) return fail(ctx, FRI_EINVAL, "null argument");
+    uint32_t log_N = 0;
+    while (((size_t)1 << log_N) < n) log_N++;
+    if (log_N > 17 || log_N > ctx->log_n_max)
+        return fail(ctx, FRI_EINVAL, "arbitrary-point interpolation is O(n^2): n <= 2^17 and <= 2^log_n_max");
+    if (!check_canonical(xs, n) || !check_canonical(ys, n)) return fail(ctx, FRI_EINVAL, "value not canonical (>= p)");
+    *len_out = 0;
+    if (n == 0) return FRI_OK;                                   // Polynomial::zero() (interpolation.rs:133-136)
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const size_t N = (size_t)1 << log_N;
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, xs, n * 4, hipMemcpyHostToDevice, s));
+    launch_interp_weights(ctx->scratch_a, n, ctx->scratch_b, s);           // prod_{i!=j}(x_j - x_i)
+    launch_batch_inverse(ctx->scratch_b, ctx->scratch_c, n, 1, s);          // w_j (Montgomery; 0 -> 0)
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_b, ys, n * 4, hipMemcpyHostToDevice, s));   // after the inverse (stream order)
+    launch_interp_coeffs(ctx->scratch_b, ctx->scratch_c, n, s);             // c_j = y_j w_j
+    launch_interp_eval(ctx->scratch_a, ctx->scratch_c, n, log_N, ctx->scratch_b, s);   // f(w_N^k), k < N
+    NttPlan p{};
+    p.log_n = log_N;
+    p.tw = ctx->tw_inv;
+    launch_pow_table(ctx->pow_lo, ctx->pow_hi, log_N, 1u, inv_std((uint32_t)(N % P)), s);   // N^-1
+    p.post_lo = ctx->pow_lo;
+    p.post_hi = ctx->pow_hi;
+    launch_ntt(p, ctx->scratch_b, N, ctx->scratch_a, s);
+    FRI_HIP(ctx, hipGetLastError());
+    FRI_HIP(ctx, hipMemcpyAsync(coeffs_out, ctx->scratch_a, n * 4, hipMemcpyDeviceToHost, s));   // deg f < n
+    FRI_HIP(ctx, hipStreamSynchronize(s));
+    size_t len = n;
+    while (len > 0 && coeffs_out[len - 1] == 0) len--;          // Polynomial::new trim (ops.rs:19-37)
+    *len_out = len;
+    return FRI_OK;
+}
+
 extern "C" int fri_evaluate(fri_ctx* ctx, const uint32_t* coeffs, size_t d, const uint32_t* xs, size_t count,
                             uint32_t* out) {
     if (!ctx || (d && !coeffs) || (count && (!xs || !out))) return fail(ctx, FRI_EINVAL, "null argument");

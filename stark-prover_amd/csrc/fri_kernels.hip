@@ -438,6 +438,80 @@ void launch_evaluate(const uint32_t* coeffs, size_t d, const uint32_t* xs, size_
     hipLaunchKernelGGL(k_evaluate, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, coeffs, d, xs, count, out);
 }
 
+// ============================================ arbitrary-point interpolate ==
+// Polynomial::interpolate on points that are not a coset (interpolation.rs:
+// 121-152): f = sum_j y_j w_j Z(x)/(x - x_j), w_j = 1/prod_{i!=j}(x_j - x_i).
+// Products run in the "R^-1 per step" form: mmul(acc, t) = acc*t*R^-1 with
+// both operands canonical, so a chain of m products carries R^-m, fixed by one
+// product with R^(m+1) at the end.  x and c tiles are staged in LDS.
+constexpr uint32_t INTERP_TILE = 1024;
+
+__global__ __launch_bounds__(256) void k_interp_weights(const uint32_t* __restrict__ xs, size_t n,
+                                                        uint32_t* __restrict__ acc, uint32_t fix) {
+    __shared__ uint32_t xt[INTERP_TILE];
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t xj = j < n ? xs[j] : 0u;
+    uint32_t a = 1u;
+    for (size_t base = 0; base < n; base += INTERP_TILE) {
+        const uint32_t m = (uint32_t)(n - base < INTERP_TILE ? n - base : INTERP_TILE);
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) xt[i] = xs[base + i];
+        __syncthreads();
+        const uint32_t self = (j >= base && j < base + m) ? (uint32_t)(j - base) : INTERP_TILE;
+        for (uint32_t i = 0; i < m; i++) {
+            const uint32_t t = i == self ? R_MOD_P : sub(xj, xt[i]);   // skip i == j: a Montgomery 1
+            a = mmul(a, t);
+        }
+    }
+    if (j < n) acc[j] = mmul(a, fix);            // * R^(n-1): prod_{i!=j}(x_j - x_i), canonical
+}
+void launch_interp_weights(const uint32_t* xs, size_t n, uint32_t* acc, hipStream_t s) {
+    const uint32_t fix = pow_std(R_MOD_P, (uint64_t)n);                       // R^n: mmul(a, R^n) = a R^(n-1)
+    hipLaunchKernelGGL(k_interp_weights, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, xs, n, acc, fix);
+}
+
+__global__ void k_interp_coeffs(const uint32_t* __restrict__ ys, uint32_t* __restrict__ w, size_t n) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) w[j] = mmul(ys[j], w[j]);        // w Montgomery -> c_j = y_j w_j canonical
+}
+void launch_interp_coeffs(const uint32_t* ys, uint32_t* w_to_c, size_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_interp_coeffs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ys, w_to_c, n);
+}
+
+// f(u), u = w_N^k: num/den = sum_{j<J} c_j/(u - x_j) as one running fraction,
+// num <- num (u - x_j) + c_j den, den <- den (u - x_j).  After all n points
+// den = Z(u) and num = Z(u) * sum_j c_j/(u - x_j) = f(u): a polynomial
+// identity in u, so it holds at u = x_j too (no inverse, no special case).
+__global__ __launch_bounds__(256) void k_interp_eval(const uint32_t* __restrict__ xs, const uint32_t* __restrict__ c,
+                                                     size_t n, uint32_t w_m, uint32_t fix, uint32_t* __restrict__ f,
+                                                     size_t N) {
+    __shared__ uint2 tile[INTERP_TILE];
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t u = from_mont(mpow(w_m, k));
+    uint32_t num = 0u, den = 1u;
+    for (size_t base = 0; base < n; base += INTERP_TILE) {
+        const uint32_t m = (uint32_t)(n - base < INTERP_TILE ? n - base : INTERP_TILE);
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) tile[i] = make_uint2(xs[base + i], c[base + i]);
+        __syncthreads();
+#pragma unroll 4
+        for (uint32_t i = 0; i < m; i++) {
+            const uint2 xc = tile[i];
+            const uint32_t t = sub(u, xc.x);
+            num = add(mmul(num, t), mmul(xc.y, den));
+            den = mmul(den, t);
+        }
+    }
+    if (k < N) f[k] = mmul(num, fix);            // * R^n (n steps of R^-1)
+}
+void launch_interp_eval(const uint32_t* xs, const uint32_t* c, size_t n, uint32_t log_N, uint32_t* f,
+                        hipStream_t s) {
+    const size_t N = (size_t)1 << log_N;
+    const uint32_t fix = pow_std(R_MOD_P, (uint64_t)n + 1);                   // mmul(num, R^(n+1)) = num R^n
+    hipLaunchKernelGGL(k_interp_eval, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, xs, c, n,
+                       to_mont(root_of_unity(log_N)), fix, f, N);
+}
+
 // ================================================================== fold ==
 // L'[i] = 2^-1 * ((a+b) + beta*(a-b)*x_i^-1),  a = L[i], b = L[i+m/2] = L(-x_i).
 // xinv_m[i] = Montgomery(x_i^-1) for the layer's domain.

@@ -638,16 +638,41 @@ std::vector<FE> evaluate_on_coset(const Poly& poly, const Coset& coset) {
     return to_fe(out.data(), n);
 }
 
+namespace {
+// xs == offset * w_n^i for every i (natural order, n a power of two)?
+bool is_coset(const std::vector<FE>& xs, FE* offset, uint32_t* log_n) {
+    const size_t n = xs.size();
+    if (n == 0 || (n & (n - 1)) || xs[0] == FE::zero()) return false;
+    *log_n = ceil_log2(n);
+    *offset = xs[0];
+    const FE w = omega(*log_n);
+    FE x = xs[0];
+    for (size_t i = 1; i < n; i++) {
+        x = x * w;
+        if (xs[i] != x) return false;
+    }
+    return true;
+}
+}  // namespace
+
 Poly interpolate(const std::vector<FE>& xs, const std::vector<FE>& ys) {
     if (xs.size() != ys.size()) throw Panic("xs and ys must have the same length (interpolation.rs:127)");
+    if (xs.empty()) return Poly();                              // Polynomial::zero() (interpolation.rs:133-136)
     FE offset;
-    const uint32_t log_n = coset_log_n(xs, &offset);
-    auto gpu = Gpu::thread_default(log_n);
+    uint32_t log_n = 0;
     auto y = to_u32(ys);
     std::vector<uint32_t> c(xs.size());
     size_t len = 0;
-    gpu->check(fri_interpolate(gpu->ctx(), y.data(), log_n, static_cast<uint32_t>(offset.value()), c.data(), &len),
-               "fri_interpolate");
+    if (is_coset(xs, &offset, &log_n)) {                        // iNTT on the coset
+        auto gpu = Gpu::thread_default(log_n);
+        gpu->check(fri_interpolate(gpu->ctx(), y.data(), log_n, static_cast<uint32_t>(offset.value()), c.data(), &len),
+                   "fri_interpolate");
+    } else {                                                    // any other point set: O(n^2) on the device
+        auto gpu = Gpu::thread_default(ceil_log2(xs.size()));
+        auto x = to_u32(xs);
+        gpu->check(fri_interpolate_points(gpu->ctx(), x.data(), y.data(), x.size(), c.data(), &len),
+                   "fri_interpolate_points");
+    }
     return Poly(to_fe(c.data(), len));
 }
 

@@ -384,7 +384,8 @@ bool verify_fibsq(const std::vector<std::vector<uint8_t>>& messages, FE a_last, 
 // ---------------------------------------------------- polynomial layer (GPU)
 // evaluate() at every coset point (fri_commit.rs:78): the LDE.
 std::vector<FE> evaluate_on_coset(const Poly& poly, const Coset& coset);
-// Polynomial::interpolate (ops.rs:239-241) for xs = a coset offset*<omega_n>.
+// Polynomial::interpolate (ops.rs:239-241): the iNTT when xs is a coset
+// offset*<omega_n> in natural order, fri_interpolate_points otherwise.
 Poly interpolate(const std::vector<FE>& xs, const std::vector<FE>& ys);
 // Element-wise inverse with inverse(0) = 0 (element.rs:54-57).
 std::vector<FE> batch_inverse(const std::vector<FE>& xs);

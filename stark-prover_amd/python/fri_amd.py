@@ -90,6 +90,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_batch_inverse": (i32, [vp, pu32, pu32, sz]),
         "fri_lde": (i32, [vp, pu32, sz, u32, u32, pu32]),
         "fri_interpolate": (i32, [vp, pu32, u32, u32, pu32, ctypes.POINTER(sz)]),
+        "fri_interpolate_points": (i32, [vp, pu32, pu32, sz, pu32, ctypes.POINTER(sz)]),
         "fri_evaluate": (i32, [vp, pu32, sz, pu32, sz, pu32]),
         "fri_fold": (i32, [vp, pu32, u32, u32, u32, pu32]),
         "fri_merkle_root": (i32, [vp, pu32, sz, ctypes.c_char_p]),
@@ -196,6 +197,17 @@ class Context:
         out = np.empty(y.size, dtype=np.uint32)
         ln = ctypes.c_size_t()
         self._check(self.lib.fri_interpolate(self.h, _ptr(y), log_n, offset, _ptr(out), ctypes.byref(ln)))
+        return out[: ln.value]
+
+    def interpolate_points(self, xs, ys) -> np.ndarray:
+        """Polynomial::interpolate(xs, ys) on arbitrary points
+        (interpolation.rs:121-152; fri_interpolate_points), trimmed."""
+        x, y = _u32(xs), _u32(ys)
+        if x.size != y.size:
+            raise FriError(FRI_EINVAL, "Mismatched x and y lengths")   # interpolation.rs:127-133 panics
+        out = np.empty(max(1, x.size), dtype=np.uint32)
+        ln = ctypes.c_size_t()
+        self._check(self.lib.fri_interpolate_points(self.h, _ptr(x), _ptr(y), x.size, _ptr(out), ctypes.byref(ln)))
         return out[: ln.value]
 
     def evaluate(self, coeffs, xs) -> np.ndarray:

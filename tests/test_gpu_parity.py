@@ -104,6 +104,63 @@ def test_interpolate_roundtrip(ctx, corc, log_n):
     assert np.array_equal(got.astype(np.uint64), want[:ln])
 
 
+@pytest.mark.parametrize("n,seed,dups", [(1, 1, 0), (2, 2, 0), (3, 3, 1), (5, 4, 0), (7, 5, 2), (16, 6, 0),
+                                         (17, 7, 3), (33, 8, 0), (40, 9, 5)])
+def test_interpolate_points_matches_lagrange(ctx, oracle, n, seed, dups):
+    """Polynomial::interpolate on arbitrary points (interpolation.rs:121-152,
+    fri_interpolate_points) against the twin's restatement of the reference's
+    Lagrange sum, duplicate points (whose basis polynomials vanish through
+    inverse(0) = 0) and zero values included."""
+    r = np.random.default_rng(seed)
+    xs = [int(v) for v in r.integers(0, P, n)]
+    for i in range(dups):
+        xs[int(r.integers(0, n))] = xs[int(r.integers(0, n))]
+    ys = [int(v) for v in r.integers(0, P, n)]
+    if n > 2:
+        ys[1] = 0
+    got = ctx.interpolate_points(xs, ys)
+    want = oracle.interpolate_lagrange_polynomials(xs, ys, P)
+    assert got.tolist() == want
+
+
+@pytest.mark.parametrize("n", [100, 1000, 4096, 5000])
+def test_interpolate_points_matches_c_oracle(ctx, corc, n):
+    """Larger arbitrary point sets against the C oracle's Lagrange sum; the
+    result evaluates back to ys at every point."""
+    r = np.random.default_rng(n)
+    xs = np.unique(r.integers(0, P, n + 64, dtype=np.uint64))[:n]
+    r.shuffle(xs)
+    ys = r.integers(0, P, n, dtype=np.uint64)
+    got = ctx.interpolate_points(xs, ys)
+    want = np.empty(n, dtype=np.uint64)
+    ln = corc.orc_interpolate_lagrange(xs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                       ys.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n,
+                                       want.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), P)
+    assert np.array_equal(got.astype(np.uint64), want[:ln])
+    assert np.array_equal(ctx.evaluate(got, xs).astype(np.uint64), ys)
+
+
+def test_interpolate_points_on_coset_equals_intt(ctx):
+    """On a coset the O(n^2) path and the iNTT path give the same polynomial."""
+    log_n = 10
+    c = rng_field(77, 1 << log_n)
+    ys = ctx.lde(c, log_n, 5)
+    w = pow(5, (P - 1) >> log_n, P)
+    xs = [5 * pow(w, i, P) % P for i in range(1 << log_n)]
+    assert np.array_equal(ctx.interpolate_points(xs, ys), ctx.interpolate(ys, 5))
+
+
+def test_interpolate_points_edges(ctx):
+    import fri_amd
+    assert ctx.interpolate_points([], []).tolist() == []                     # Polynomial::zero()
+    assert ctx.interpolate_points([7], [0]).tolist() == []
+    assert ctx.interpolate_points([7], [9]).tolist() == [9]
+    with pytest.raises(fri_amd.FriError):
+        ctx.interpolate_points([1, 2], [3])                                  # interpolation.rs:127 panics
+    with pytest.raises(fri_amd.FriError):
+        ctx.interpolate_points([P], [1])                                     # not canonical
+
+
 def test_interpolate_matches_lagrange(ctx, corc, oracle):
     """Same interpolant as the reference's Lagrange path (interpolation.rs:121-152)."""
     log_n = 4
