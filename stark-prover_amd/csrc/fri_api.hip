@@ -108,6 +108,8 @@ struct fri_ctx {
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
     uint64_t commit_gen = 0;        // bumped by every commit: read-backs of an older proof are refused
     uint32_t commit_log_n = 0;      // codeword log2 of the resident commit
+    uint32_t* interp_tmp = nullptr; // fri_interpolate_points segment partials (allocated on first use)
+    size_t interp_cap = 0;
     uint32_t* dq_host = nullptr;    // decommitment gather output: 64 KiB of coherent pinned host
     uint32_t* dq_dev = nullptr;     // memory the gather kernel writes directly (its device address)
     uint32_t* trace_tree = nullptr; // Merkle tree of the last fri_trace_commit LDE
@@ -246,6 +248,7 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     hipFree(ctx->pow_lo); hipFree(ctx->pow_hi);
     hipFree(ctx->d_state);
     if (ctx->dq_host) hipHostFree(ctx->dq_host);
+    if (ctx->interp_tmp) hipFree(ctx->interp_tmp);
     hipFree(ctx->trace_tree);
     hipFree(ctx->trace_lde);
     if (ctx->h_state) hipHostFree(ctx->h_state);
@@ -344,12 +347,21 @@ extern "C" int fri_interpolate_points(fri_ctx* ctx, const uint32_t* xs, const ui
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const size_t N = (size_t)1 << log_N;
+    const size_t tw = interp_tmp_words(n, log_N);
+    if (tw > ctx->interp_cap) {
+        FRI_HIP(ctx, hipStreamSynchronize(s));
+        if (ctx->interp_tmp) hipFree(ctx->interp_tmp);
+        ctx->interp_tmp = nullptr;
+        ctx->interp_cap = 0;
+        if (hipMalloc(&ctx->interp_tmp, tw * 4) != hipSuccess) return fail(ctx, FRI_ENOMEM, "interpolation scratch");
+        ctx->interp_cap = tw;
+    }
     FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, xs, n * 4, hipMemcpyHostToDevice, s));
-    launch_interp_weights(ctx->scratch_a, n, ctx->scratch_b, s);           // prod_{i!=j}(x_j - x_i)
+    launch_interp_weights(ctx->scratch_a, n, ctx->scratch_b, ctx->interp_tmp, s);   // prod_{i!=j}(x_j - x_i)
     launch_batch_inverse(ctx->scratch_b, ctx->scratch_c, n, 1, s);          // w_j (Montgomery; 0 -> 0)
     FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_b, ys, n * 4, hipMemcpyHostToDevice, s));   // after the inverse (stream order)
     launch_interp_coeffs(ctx->scratch_b, ctx->scratch_c, n, s);             // c_j = y_j w_j
-    launch_interp_eval(ctx->scratch_a, ctx->scratch_c, n, log_N, ctx->scratch_b, s);   // f(w_N^k), k < N
+    launch_interp_eval(ctx->scratch_a, ctx->scratch_c, n, log_N, ctx->scratch_b, ctx->interp_tmp, s);   // f(w_N^k)
     NttPlan p{};
     p.log_n = log_N;
     p.tw = ctx->tw_inv;

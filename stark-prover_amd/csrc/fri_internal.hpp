@@ -74,9 +74,12 @@ void launch_coset_points(uint32_t* out, size_t count, uint32_t offset, uint32_t 
 void launch_square_mont(const uint32_t* in, uint32_t* out, size_t count, hipStream_t s);
 // Arbitrary-point interpolation (fri_interpolate_points): prod_{i!=j}(x_j - x_i)
 // into acc; c_j = y_j * w_j (w Montgomery) in place over w; f(w_N^k) for k < N.
-void launch_interp_weights(const uint32_t* xs, size_t n, uint32_t* acc, hipStream_t s);
+// tmp: interp_tmp_words(n, log_N) words of segment partials.
+size_t interp_tmp_words(size_t n, uint32_t log_N);
+void launch_interp_weights(const uint32_t* xs, size_t n, uint32_t* acc, uint32_t* tmp, hipStream_t s);
 void launch_interp_coeffs(const uint32_t* ys, uint32_t* w_to_c, size_t n, hipStream_t s);
-void launch_interp_eval(const uint32_t* xs, const uint32_t* c, size_t n, uint32_t log_N, uint32_t* f, hipStream_t s);
+void launch_interp_eval(const uint32_t* xs, const uint32_t* c, size_t n, uint32_t log_N, uint32_t* f, uint32_t* tmp,
+                        hipStream_t s);
 void launch_evaluate(const uint32_t* coeffs, size_t d, const uint32_t* xs, size_t count,
                      uint32_t* out, hipStream_t s);
 struct DecommitPlan {

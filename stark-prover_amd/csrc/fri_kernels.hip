@@ -443,17 +443,23 @@ void launch_evaluate(const uint32_t* coeffs, size_t d, const uint32_t* xs, size_
 // 121-152): f = sum_j y_j w_j Z(x)/(x - x_j), w_j = 1/prod_{i!=j}(x_j - x_i).
 // Products run in the "R^-1 per step" form: mmul(acc, t) = acc*t*R^-1 with
 // both operands canonical, so a chain of m products carries R^-m, fixed by one
-// product with R^(m+1) at the end.  x and c tiles are staged in LDS.
+// product with R^(m+1) at the end.  x and c tiles are staged in LDS.  One
+// lane per output point leaves a wave per SIMD at n = 2^16, so the point range
+// is cut into S segments (blockIdx.y) whose partial results are combined by a
+// second kernel.
 constexpr uint32_t INTERP_TILE = 1024;
 
-__global__ __launch_bounds__(256) void k_interp_weights(const uint32_t* __restrict__ xs, size_t n,
-                                                        uint32_t* __restrict__ acc, uint32_t fix) {
+// segment s of prod_{i!=j}(x_j - x_i): part[s*n + j], exponent (segment
+// length - [j in segment]) of R^-1
+__global__ __launch_bounds__(256) void k_interp_weights(const uint32_t* __restrict__ xs, size_t n, size_t seg,
+                                                        uint32_t* __restrict__ part) {
     __shared__ uint32_t xt[INTERP_TILE];
     const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t lo = (size_t)blockIdx.y * seg, hi = lo + seg < n ? lo + seg : n;
     const uint32_t xj = j < n ? xs[j] : 0u;
     uint32_t a = 1u;
-    for (size_t base = 0; base < n; base += INTERP_TILE) {
-        const uint32_t m = (uint32_t)(n - base < INTERP_TILE ? n - base : INTERP_TILE);
+    for (size_t base = lo; base < hi; base += INTERP_TILE) {
+        const uint32_t m = (uint32_t)(hi - base < INTERP_TILE ? hi - base : INTERP_TILE);
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) xt[i] = xs[base + i];
         __syncthreads();
@@ -463,11 +469,36 @@ __global__ __launch_bounds__(256) void k_interp_weights(const uint32_t* __restri
             a = mmul(a, t);
         }
     }
-    if (j < n) acc[j] = mmul(a, fix);            // * R^(n-1): prod_{i!=j}(x_j - x_i), canonical
+    if (j < n) part[blockIdx.y * n + j] = a;
 }
-void launch_interp_weights(const uint32_t* xs, size_t n, uint32_t* acc, hipStream_t s) {
-    const uint32_t fix = pow_std(R_MOD_P, (uint64_t)n);                       // R^n: mmul(a, R^n) = a R^(n-1)
-    hipLaunchKernelGGL(k_interp_weights, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, xs, n, acc, fix);
+// prod over the S segments (S - 1 more R^-1), times the fix-up: the exact
+// prod_{i!=j}(x_j - x_i), canonical
+__global__ void k_interp_weights_join(const uint32_t* __restrict__ part, size_t n, uint32_t S, uint32_t fix,
+                                      uint32_t* __restrict__ acc) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    uint32_t a = part[j];
+    for (uint32_t s = 1; s < S; s++) a = mmul(a, part[s * n + j]);
+    acc[j] = mmul(a, fix);
+}
+static uint32_t interp_segments(size_t n, size_t lanes) {
+    uint32_t S = 1;                          // >= 2^20 lanes in flight, segments of >= 256 points
+    while (S < 64 && lanes * S < ((size_t)1 << 20) && n / (2 * S) >= 256) S *= 2;
+    return S;
+}
+size_t interp_tmp_words(size_t n, uint32_t log_N) {
+    const size_t N = (size_t)1 << log_N;
+    const size_t a = interp_segments(n, n) * n, b = 2 * (size_t)interp_segments(n, N) * N;
+    return a > b ? a : b;
+}
+void launch_interp_weights(const uint32_t* xs, size_t n, uint32_t* acc, uint32_t* tmp, hipStream_t s) {
+    const uint32_t S = interp_segments(n, n);
+    const size_t seg = (n + S - 1) / S;
+    // n - 1 factors carry R^-1 (the skipped i == j does not), plus S - 1 joins
+    const uint32_t fix = pow_std(R_MOD_P, (uint64_t)n + S - 1);
+    hipLaunchKernelGGL(k_interp_weights, dim3((unsigned)((n + 255) / 256), S), dim3(256), 0, s, xs, n, seg, tmp);
+    hipLaunchKernelGGL(k_interp_weights_join, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tmp, n, S, fix,
+                       acc);
 }
 
 __global__ void k_interp_coeffs(const uint32_t* __restrict__ ys, uint32_t* __restrict__ w, size_t n) {
@@ -478,19 +509,22 @@ void launch_interp_coeffs(const uint32_t* ys, uint32_t* w_to_c, size_t n, hipStr
     hipLaunchKernelGGL(k_interp_coeffs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ys, w_to_c, n);
 }
 
-// f(u), u = w_N^k: num/den = sum_{j<J} c_j/(u - x_j) as one running fraction,
-// num <- num (u - x_j) + c_j den, den <- den (u - x_j).  After all n points
-// den = Z(u) and num = Z(u) * sum_j c_j/(u - x_j) = f(u): a polynomial
-// identity in u, so it holds at u = x_j too (no inverse, no special case).
+// f(u), u = w_N^k: num/den = sum_j c_j/(u - x_j) as one running fraction over
+// the segment's points, num <- num (u - x_j) + c_j den, den <- den (u - x_j).
+// Over all n points den = Z(u) and num = Z(u) * sum_j c_j/(u - x_j) = f(u): a
+// polynomial identity in u, so it holds at u = x_j too (no inverse, no
+// special case).  Segments are fractions over disjoint point sets and join as
+// num = num_a den_b + num_b den_a, den = den_a den_b.
 __global__ __launch_bounds__(256) void k_interp_eval(const uint32_t* __restrict__ xs, const uint32_t* __restrict__ c,
-                                                     size_t n, uint32_t w_m, uint32_t fix, uint32_t* __restrict__ f,
-                                                     size_t N) {
+                                                     size_t n, size_t seg, uint32_t w_m, size_t N,
+                                                     uint32_t* __restrict__ part) {
     __shared__ uint2 tile[INTERP_TILE];
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t lo = (size_t)blockIdx.y * seg, hi = lo + seg < n ? lo + seg : n;
     const uint32_t u = from_mont(mpow(w_m, k));
     uint32_t num = 0u, den = 1u;
-    for (size_t base = 0; base < n; base += INTERP_TILE) {
-        const uint32_t m = (uint32_t)(n - base < INTERP_TILE ? n - base : INTERP_TILE);
+    for (size_t base = lo; base < hi; base += INTERP_TILE) {
+        const uint32_t m = (uint32_t)(hi - base < INTERP_TILE ? hi - base : INTERP_TILE);
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) tile[i] = make_uint2(xs[base + i], c[base + i]);
         __syncthreads();
@@ -502,14 +536,33 @@ __global__ __launch_bounds__(256) void k_interp_eval(const uint32_t* __restrict_
             den = mmul(den, t);
         }
     }
-    if (k < N) f[k] = mmul(num, fix);            // * R^n (n steps of R^-1)
+    if (k < N) {
+        part[(2 * (size_t)blockIdx.y) * N + k] = num;
+        part[(2 * (size_t)blockIdx.y + 1) * N + k] = den;
+    }
 }
-void launch_interp_eval(const uint32_t* xs, const uint32_t* c, size_t n, uint32_t log_N, uint32_t* f,
+__global__ void k_interp_eval_join(const uint32_t* __restrict__ part, size_t N, uint32_t S, uint32_t fix,
+                                   uint32_t* __restrict__ f) {
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    uint32_t num = part[k], den = part[N + k];
+    for (uint32_t s = 1; s < S; s++) {
+        const uint32_t nb = part[2 * s * N + k], db = part[(2 * s + 1) * N + k];
+        num = add(mmul(num, db), mmul(nb, den));
+        den = mmul(den, db);
+    }
+    f[k] = mmul(num, fix);
+}
+void launch_interp_eval(const uint32_t* xs, const uint32_t* c, size_t n, uint32_t log_N, uint32_t* f, uint32_t* tmp,
                         hipStream_t s) {
     const size_t N = (size_t)1 << log_N;
-    const uint32_t fix = pow_std(R_MOD_P, (uint64_t)n + 1);                   // mmul(num, R^(n+1)) = num R^n
-    hipLaunchKernelGGL(k_interp_eval, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, xs, c, n,
-                       to_mont(root_of_unity(log_N)), fix, f, N);
+    const uint32_t S = interp_segments(n, N);
+    const size_t seg = (n + S - 1) / S;
+    // n steps and S - 1 joins of R^-1: mmul(num, R^(n+S)) = num R^(n+S-1)
+    const uint32_t fix = pow_std(R_MOD_P, (uint64_t)n + S);
+    hipLaunchKernelGGL(k_interp_eval, dim3((unsigned)((N + 255) / 256), S), dim3(256), 0, s, xs, c, n, seg,
+                       to_mont(root_of_unity(log_N)), N, tmp);
+    hipLaunchKernelGGL(k_interp_eval_join, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, tmp, N, S, fix, f);
 }
 
 // ================================================================== fold ==
