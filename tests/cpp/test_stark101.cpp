@@ -393,6 +393,31 @@ TEST(gpu, layers_lde_interpolate_merkle) {
     FriChannel ch3;
     ASSERT_PANICS(decommit_fri(1, 7, proof, ch3));
 }
+TEST(gpu, interpolate_arbitrary_points) {
+    // Polynomial::interpolate (ops.rs:239-241) on a point set that is not a
+    // coset: fri_interpolate_points.  The result passes through every point.
+    std::vector<FE> xs, ys;
+    for (uint64_t i = 0; i < 300; i++) {
+        xs.push_back(FE((i * 2654435761ull + 12345) % P));
+        ys.push_back(FE((i * i * 40503ull + 7) % P));
+    }
+    Poly f = interpolate(xs, ys);
+    ASSERT_TRUE(f.coefficients.size() <= xs.size());
+    for (size_t i = 0; i < xs.size(); i++) ASSERT_TRUE(f.evaluate(xs[i]) == ys[i]);
+    // the coset in a shuffled order takes the O(n^2) path and gives the iNTT's polynomial
+    const GoldenCase* c = nullptr;
+    for (const auto& g : GOLDEN)
+        if (std::string(g.name) == "rand_n10_s42") c = &g;
+    ASSERT_TRUE(c != nullptr);
+    Poly p = poly_of(*c);
+    Coset co = coset_of(*c);
+    auto dom = co.generate_coset_domain();
+    auto vals = evaluate_on_coset(p, co);
+    std::vector<FE> sx(dom.rbegin(), dom.rend()), sy(vals.rbegin(), vals.rend());
+    ASSERT_TRUE(interpolate(sx, sy) == interpolate(dom, vals));
+    ASSERT_TRUE(interpolate(sx, sy) == p);
+}
+
 TEST(gpu, batch_inverse_matches_fermat) {
     std::vector<FE> xs;
     for (uint64_t i = 0; i < 5000; i++) xs.push_back(FE(i * 2654435761u + (i % 7 == 0 ? 0 : 1)));
