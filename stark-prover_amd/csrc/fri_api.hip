@@ -108,7 +108,7 @@ struct fri_ctx {
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
     uint64_t commit_gen = 0;        // bumped by every commit: read-backs of an older proof are refused
     uint32_t commit_log_n = 0;      // codeword log2 of the resident commit
-    uint32_t* interp_tmp = nullptr; // fri_interpolate_points segment partials (allocated on first use)
+    uint32_t* interp_tmp = nullptr; // partials of fri_interpolate_points / fri_evaluate (allocated on first use)
     size_t interp_cap = 0;
     uint32_t* dq_host = nullptr;    // decommitment gather output: 64 KiB of coherent pinned host
     uint32_t* dq_dev = nullptr;     // memory the gather kernel writes directly (its device address)
@@ -331,6 +331,19 @@ extern "C" int fri_interpolate(fri_ctx* ctx, const uint32_t* ys, uint32_t log_n,
     return FRI_OK;
 }
 
+// Device scratch of at least `words` words for the interpolation / evaluation
+// partials (grown on demand, freed with the context).
+static int ensure_tmp(fri_ctx* ctx, size_t words) {
+    if (words <= ctx->interp_cap) return FRI_OK;
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->interp_tmp) hipFree(ctx->interp_tmp);
+    ctx->interp_tmp = nullptr;
+    ctx->interp_cap = 0;
+    if (hipMalloc(&ctx->interp_tmp, words * 4) != hipSuccess) return fail(ctx, FRI_ENOMEM, "partials scratch");
+    ctx->interp_cap = words;
+    return FRI_OK;
+}
+
 // interpolate_lagrange_polynomials (interpolation.rs:121-152) on arbitrary
 // points: weights, c_j = y_j w_j, f on the 2^k-th roots of unity, iNTT
 // (fri_kernels.hip "arbitrary-point interpolate").
@@ -347,15 +360,8 @@ extern "C" int fri_interpolate_points(fri_ctx* ctx, const uint32_t* xs, const ui
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const size_t N = (size_t)1 << log_N;
-    const size_t tw = interp_tmp_words(n, log_N);
-    if (tw > ctx->interp_cap) {
-        FRI_HIP(ctx, hipStreamSynchronize(s));
-        if (ctx->interp_tmp) hipFree(ctx->interp_tmp);
-        ctx->interp_tmp = nullptr;
-        ctx->interp_cap = 0;
-        if (hipMalloc(&ctx->interp_tmp, tw * 4) != hipSuccess) return fail(ctx, FRI_ENOMEM, "interpolation scratch");
-        ctx->interp_cap = tw;
-    }
+    int rc = ensure_tmp(ctx, interp_tmp_words(n, log_N));
+    if (rc) return rc;
     FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, xs, n * 4, hipMemcpyHostToDevice, s));
     launch_interp_weights(ctx->scratch_a, n, ctx->scratch_b, ctx->interp_tmp, s);   // prod_{i!=j}(x_j - x_i)
     launch_batch_inverse(ctx->scratch_b, ctx->scratch_c, n, 1, s);          // w_j (Montgomery; 0 -> 0)
@@ -388,7 +394,12 @@ extern "C" int fri_evaluate(fri_ctx* ctx, const uint32_t* coeffs, size_t d, cons
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     if (d) FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, coeffs, d * 4, hipMemcpyHostToDevice, ctx->stream));
     if (count) FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_b, xs, count * 4, hipMemcpyHostToDevice, ctx->stream));
-    launch_evaluate(ctx->scratch_a, d, ctx->scratch_b, count, ctx->scratch_c, ctx->stream);
+    const size_t tw = evaluate_tmp_words(d, count);
+    if (tw) {
+        const int rc = ensure_tmp(ctx, tw);
+        if (rc) return rc;
+    }
+    launch_evaluate(ctx->scratch_a, d, ctx->scratch_b, count, ctx->scratch_c, ctx->interp_tmp, ctx->stream);
     FRI_HIP(ctx, hipGetLastError());
     if (count) FRI_HIP(ctx, hipMemcpyAsync(out, ctx->scratch_c, count * 4, hipMemcpyDeviceToHost, ctx->stream));
     FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));

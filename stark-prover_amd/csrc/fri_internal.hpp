@@ -80,8 +80,11 @@ void launch_interp_weights(const uint32_t* xs, size_t n, uint32_t* acc, uint32_t
 void launch_interp_coeffs(const uint32_t* ys, uint32_t* w_to_c, size_t n, hipStream_t s);
 void launch_interp_eval(const uint32_t* xs, const uint32_t* c, size_t n, uint32_t log_N, uint32_t* f, uint32_t* tmp,
                         hipStream_t s);
-void launch_evaluate(const uint32_t* coeffs, size_t d, const uint32_t* xs, size_t count,
-                     uint32_t* out, hipStream_t s);
+// Horner at arbitrary points; with few points and many coefficients (tmp of
+// evaluate_tmp_words(d, count) > 0 words) the coefficients are split over lanes.
+size_t evaluate_tmp_words(size_t d, size_t count);
+void launch_evaluate(const uint32_t* coeffs, size_t d, const uint32_t* xs, size_t count, uint32_t* out,
+                     uint32_t* tmp, hipStream_t s);
 struct DecommitPlan {
     uint64_t index;
     uint32_t log_n, n_layers;

@@ -432,10 +432,56 @@ __global__ void k_evaluate(const uint32_t* __restrict__ c, size_t d, const uint3
     for (size_t k = d; k-- > 0;) r = add(mmul(r, xm), c[k]);
     out[i] = r;
 }
+// Few points, many coefficients: lane l of the S lanes of a point takes the
+// coefficients j = k S + l (coalesced across lanes) and evaluates
+// H_l = sum_k c[kS + l] (x^S)^k by Horner in y = x^S; then
+// p(x) = sum_l x^l H_l, summed per workgroup here and over the B workgroups
+// of the point by k_evaluate_join.  Exact field arithmetic: the same value as
+// Horner's rule in any order.
+__global__ __launch_bounds__(256) void k_evaluate_strided(const uint32_t* __restrict__ c, size_t d,
+                                                          const uint32_t* __restrict__ xs, uint32_t S,
+                                                          uint32_t* __restrict__ part) {
+    __shared__ uint32_t red[4];
+    const uint32_t p = blockIdx.y, l = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t xm = to_mont(xs[p]);
+    const uint32_t ym = mpow(xm, S);                               // x^S, Montgomery
+    const size_t K = (d + S - 1) / S;
+    uint32_t h = 0;
+    for (size_t k = K; k-- > 0;) {
+        const size_t j = k * S + l;
+        h = add(mmul(h, ym), j < d ? c[j] : 0u);
+    }
+    uint32_t v = mmul(h, mpow(xm, l));                             // x^l H_l, canonical
+    for (int o = 32; o >= 1; o >>= 1) v = add(v, (uint32_t)__shfl_xor((int)v, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) part[(size_t)p * gridDim.x + blockIdx.x] = add(add(red[0], red[1]), add(red[2], red[3]));
+}
+__global__ void k_evaluate_join(const uint32_t* __restrict__ part, uint32_t B, size_t count, uint32_t* __restrict__ out) {
+    const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= count) return;
+    uint32_t v = 0;
+    for (uint32_t b = 0; b < B; b++) v = add(v, part[p * B + b]);
+    out[p] = v;
+}
+size_t evaluate_tmp_words(size_t d, size_t count) {
+    if (count >= ((size_t)1 << 16) || d < 4096) return 0;          // one lane per point is enough
+    size_t S = 256;                                                // >= 2^18 lanes, >= 16 coefficients each
+    while (S < 8192 && count * S < ((size_t)1 << 18) && d / (2 * S) >= 16) S *= 2;
+    return count * (S / 256);
+}
 void launch_evaluate(const uint32_t* coeffs, size_t d, const uint32_t* xs, size_t count, uint32_t* out,
-                     hipStream_t s) {
+                     uint32_t* tmp, hipStream_t s) {
     if (!count) return;
-    hipLaunchKernelGGL(k_evaluate, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, coeffs, d, xs, count, out);
+    const size_t tw = evaluate_tmp_words(d, count);
+    if (!tw) {
+        hipLaunchKernelGGL(k_evaluate, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, coeffs, d, xs, count,
+                           out);
+        return;
+    }
+    const uint32_t B = (uint32_t)(tw / count), S = 256 * B;
+    hipLaunchKernelGGL(k_evaluate_strided, dim3(B, (unsigned)count), dim3(256), 0, s, coeffs, d, xs, S, tmp);
+    hipLaunchKernelGGL(k_evaluate_join, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, tmp, B, count, out);
 }
 
 // ============================================ arbitrary-point interpolate ==

@@ -87,6 +87,24 @@ def test_evaluate_matches_horner(ctx, corc):
     assert ctx.evaluate([5], [0]).tolist() == [5]          # constant (ops.rs:568-574)
 
 
+@pytest.mark.parametrize("d,count", [(1 << 21, 1), (5000, 1), (4096, 3), ((1 << 16) + 3, 100), (1 << 20, 7),
+                                     (100000, 2000)])
+def test_evaluate_few_points_many_coefficients(ctx, corc, d, count):
+    """Polynomial::evaluate (ops.rs:76-83) with the coefficients split over
+    lanes (few points, many coefficients: the reference's bench_eval shape,
+    benches/poly_ops.rs:161-181, at prover sizes) against Horner in the C oracle;
+    x = 0, 1 and p - 1 included."""
+    c = rng_field(d + count, d)
+    xs = rng_field(count * 7 + 1, count)
+    xs[0] = 0
+    if count > 2:
+        xs[1], xs[2] = 1, P - 1
+    got = ctx.evaluate(c, xs)
+    cs, pc = c_u64(c)
+    for i in range(count) if count <= 8 else list(range(4)) + list(range(count - 4, count)) + [count // 2]:
+        assert int(got[i]) == corc.orc_poly_evaluate(pc, d, int(xs[i]), P), i
+
+
 # ------------------------------------------------------ poly: interpolate --
 @pytest.mark.parametrize("log_n", [0, 1, 2, 5, 10, 13, 16])
 def test_interpolate_roundtrip(ctx, corc, log_n):
