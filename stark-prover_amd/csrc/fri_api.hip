@@ -108,7 +108,7 @@ struct fri_ctx {
     uint32_t sharded_layers = 0;    // layers of the last commit held block-wise across ranks
     uint64_t commit_gen = 0;        // bumped by every commit: read-backs of an older proof are refused
     uint32_t commit_log_n = 0;      // codeword log2 of the resident commit
-    uint32_t* interp_tmp = nullptr; // partials of fri_interpolate_points / fri_evaluate (allocated on first use)
+    uint32_t* interp_tmp = nullptr; // partials of fri_interpolate_points / fri_evaluate, fri_merkle_root's tree (grown on use)
     size_t interp_cap = 0;
     uint32_t* dq_host = nullptr;    // decommitment gather output: 64 KiB of coherent pinned host
     uint32_t* dq_dev = nullptr;     // memory the gather kernel writes directly (its device address)
@@ -521,13 +521,17 @@ extern "C" int fri_merkle_root(fri_ctx* ctx, const uint32_t* values, size_t n, u
     if (!check_canonical(values, n)) return fail(ctx, FRI_EINVAL, "value not canonical (>= p)");
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     FRI_HIP(ctx, hipMemcpyAsync(ctx->scratch_a, values, n * 4, hipMemcpyHostToDevice, ctx->stream));
+    // the tree lives in the context's partials scratch (no hipMalloc / hipFree,
+    // which synchronises the device, per MerkleTree::new)
     uint32_t* root_dev;
     uint32_t* tree = nullptr;
     bool pow2 = (n & (n - 1)) == 0;
     if (pow2) {
         uint32_t L = 0;
         while (((size_t)1 << L) < n) L++;
-        FRI_HIP(ctx, hipMalloc(&tree, (((size_t)2 << L)) * 32));
+        const int rc = ensure_tmp(ctx, ((size_t)2 << L) * 8);
+        if (rc) return rc;
+        tree = ctx->interp_tmp;
         LayerTask t{};
         t.values = ctx->scratch_a;
         t.tree = tree;
@@ -537,7 +541,9 @@ extern "C" int fri_merkle_root(fri_ctx* ctx, const uint32_t* values, size_t n, u
     } else {
         size_t total = 0;
         for (size_t m = n;; m = (m + 1) / 2) { total += m; if (m == 1) break; }
-        FRI_HIP(ctx, hipMalloc(&tree, total * 32));
+        const int rc = ensure_tmp(ctx, total * 8);
+        if (rc) return rc;
+        tree = ctx->interp_tmp;
         uint32_t* cur = tree;
         hipLaunchKernelGGL(k_leaf_generic, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
                            ctx->scratch_a, cur, n);
@@ -556,7 +562,6 @@ extern "C" int fri_merkle_root(fri_ctx* ctx, const uint32_t* values, size_t n, u
     uint32_t w[8];
     hipError_t e1 = hipMemcpyAsync(w, root_dev, 32, hipMemcpyDeviceToHost, ctx->stream);
     hipError_t e2 = hipStreamSynchronize(ctx->stream);
-    hipFree(tree);
     FRI_HIP(ctx, e1);
     FRI_HIP(ctx, e2);
     digest_to_bytes(w, root32);
