@@ -77,6 +77,24 @@ def _same(a, b):
             and bytes(a.channel_out.digest) == bytes(b.channel_out.digest))
 
 
+def _expected(log_n, blowup_log):
+    """Oracle transcript of the bench workload (tests/golden/bench_transcripts.json,
+    written by tests/golden/make_bench_transcripts.py from the C oracle), or None."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "bench_transcripts.json")) as f:
+            return json.load(f).get(f"{log_n}/42/{blowup_log}")
+    except (OSError, ValueError):
+        return None
+
+
+def _matches(res, exp):
+    return (res.n_layers == len(exp["roots"]) and res.n_rounds == len(exp["betas"])
+            and [bytes(res.roots[k]).hex() for k in range(res.n_layers)] == exp["roots"]
+            and [int(res.betas[i]) for i in range(res.n_rounds)] == exp["betas"]
+            and int(res.final_value) == exp["final_value"] and int(res.final_degree) == exp["final_degree"]
+            and bytes(res.channel_out.digest).hex() == exp["state"])
+
+
 def main():
     # The contract's ONE JSON line goes to the original stdout; everything
     # else written to fd 1 by native libraries (gloo connection messages, the
@@ -88,16 +106,23 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--log-n", type=int, default=24, help="codeword log2 per GPU (weak scaling)")
+    ap.add_argument("--log-n", type=int, default=None,
+                    help="N=1: codeword log2 (default 24).  N>1: with --scaling strong the fixed codeword "
+                         "(default 28 = configs[4]); with --scaling weak the log2 per GPU (default 24)")
+    ap.add_argument("--scaling", choices=("auto", "strong", "weak"), default="auto",
+                    help="N>1: strong = one fixed codeword over the N ranks; weak = 2^log_n per GPU. "
+                         "auto: strong at 2^28 (BASELINE configs[4]), or weak when --log-n is given")
     ap.add_argument("--blowup-log", type=int, default=3)
     ap.add_argument("--mode", choices=("sharded", "replicas"), default="sharded",
-                    help="N>1: one coset-sharded codeword of 2^(log_n+log2 N) (default), or N independent commits")
+                    help="N>1: one coset-sharded codeword (default), or N independent 2^24 commits")
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                     help="sharded data path: the library's RCCL communicator, or host-staged gloo (rehearsal only)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="N>1: skip the secondary scaling points (weak 2^24 per GPU, strong 2^24)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the side measurements (PCIe-inclusive, serving, prover): A/B timing runs")
+                    help="skip the side measurements (PCIe-inclusive, serving, prover, 2^28): A/B timing runs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -122,18 +147,53 @@ def main():
     mode = args.mode if world > 1 else "single"
     if world > 1 and (1 << logG) != world:
         mode = "replicas"                                   # sharding needs a power-of-two world
-    log_n = args.log_n + (logG if mode == "sharded" else 0)   # codeword committed by the job (sharded) / rank
-    d = 1 << (log_n - args.blowup_log)
-    ctx = fri_amd.Context(device, log_n)
+    scaling = "weak"
+    if mode == "sharded":
+        scaling = args.scaling if args.scaling != "auto" else ("weak" if args.log_n is not None else "strong")
     note = None
+    fallback = None
 
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(step, steps, warmup):
+        for _ in range(warmup):
+            step()
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        barrier_sync()
+        return max_over_ranks(time.perf_counter() - t0)
+
+    res = fri_amd.CommitResult()
+    secondary = {}
+    dist_report = None
     if mode == "sharded":
         import torch
+        log_n = (args.log_n or 28) if scaling == "strong" else (args.log_n or 24) + logG
+        points = [(f"{scaling}_primary", log_n)]
+        if not args.no_secondary:
+            for name, L in (("weak_2p24_per_gpu", 24 + logG), ("strong_2p24", 24)):
+                if L != log_n:
+                    points.insert(0, (name, L))              # secondaries first: the primary's plan stays resident
+        ctx = fri_amd.Context(device, max(L for _, L in points) - logG)   # shard-sized (fri_amd.h)
         uid = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
             uid = torch.frombuffer(bytearray(fri_amd.Context.unique_id()), dtype=torch.uint8).clone()
         dist.broadcast(uid, 0)
-        coeffs = _coeffs(42, d, fri_amd.P)                    # one polynomial for the whole job
 
         def agreed(step):
             """Run one step of the sharded setup; every rank learns whether ALL
@@ -143,7 +203,7 @@ def main():
             ok = 1
             try:
                 if step() is False:
-                    ok, note = 0, note or "sharded transcript differed from the 1-GPU commit"
+                    ok, note = 0, note or "sharded transcript differed from the C oracle's"
             except fri_amd.FriError as e:
                 ok, note = 0, f"sharded path failed: {e}"
             flag = torch.tensor([ok], dtype=torch.int32)
@@ -160,19 +220,51 @@ def main():
                 ctx.attach_rccl(rank, world, bytes(uid.numpy()))
             attached = True
 
-        res0 = None
+        ok = agreed(attach) and agreed(lambda: ctx.dist_selftest(4096))   # transport sanity first
+        if ok:
+            r_rank, r_world, r_kind = ctx.dist_info()
+            dist_report = {"transport": r_kind, "world_reported": r_world, "rank_reported": r_rank}
+        for name, L in points:
+            if not ok:
+                break
+            dL = 1 << (L - args.blowup_log)
+            cf = _coeffs(42, dL, fri_amd.P)                     # one polynomial for the whole job
+            exp = _expected(L, args.blowup_log)
+            first = fri_amd.CommitResult()
 
-        def first_commit():
-            nonlocal res0
-            res0 = ctx.commit_sharded(coeffs, log_n)
-            # the sharded transcript must equal this rank's own 1-GPU commit
-            return _same(res0, ctx.commit(coeffs, log_n))
+            def first_commit():
+                first_ = ctx.commit_sharded(cf, L)
+                ctypes.memmove(ctypes.byref(first), ctypes.byref(first_), ctypes.sizeof(first))
+                return True if exp is None else _matches(first_, exp)
 
-        ok = (agreed(attach) and agreed(lambda: ctx.dist_selftest(4096))   # transport sanity first
-              and agreed(first_commit))
+            if not agreed(first_commit):
+                if name.endswith("_primary"):
+                    ok = False
+                else:
+                    secondary[name] = {"error": note}
+                    note = None
+                    ok = ctx.dist_info()[2] != "none"              # an aborted transport ends the sharded run
+                continue
+            dptr = ctypes.c_void_p()
+            ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, dL, ctypes.byref(dptr)))
+            out = fri_amd.CommitResult() if not name.endswith("_primary") else res
+
+            def sstep(dptr=dptr, dL=dL, L=L, out=out):
+                ctx._check(ctx.lib.fri_commit_sharded_device(ctx.h, dptr, dL, L, fri_amd.GENERATOR, None, 0, None,
+                                                              ctypes.byref(out)))
+
+            if name.endswith("_primary"):
+                res0, d, coeffs, step = first, dL, cf, sstep
+                verified = exp is not None
+                break
+            k = max(3, args.steps // 4)
+            el = timed(sstep, k, 1)
+            secondary[name] = {"codeword_log2": L, "per_gpu_log2": L - logG, "ms_per_step": round(1000 * el / k, 4),
+                               "value": round((1 << L) * k / el, 1), "unit": "field-elems/s", "steps": k,
+                               "oracle_verified": exp is not None and _same(out, first) and _matches(out, exp)}
         if not ok:
-            note = note or "another rank failed during the sharded setup"
-            print(f"[bench] rank {rank}: {note}; falling back to replicas", file=sys.stderr, flush=True)
+            fallback = note or "another rank failed during the sharded setup"
+            print(f"[bench] rank {rank}: {fallback}; falling back to replicas", file=sys.stderr, flush=True)
             if attached:
                 try:
                     ctx.detach()
@@ -180,52 +272,35 @@ def main():
                     pass
             ctx.close()
             mode = "replicas"
-            log_n = args.log_n
-            d = 1 << (log_n - args.blowup_log)
-            ctx = fri_amd.Context(device, log_n)
+            scaling = "weak"
+            secondary = {}
     if mode != "sharded":
-        coeffs = _coeffs(42 + rank, d, fri_amd.P)             # replicas: an independent codeword per rank
+        log_n = args.log_n or 24
+        d = 1 << (log_n - args.blowup_log)
+        ctx = fri_amd.Context(device, log_n)
+        coeffs = _coeffs(42 + (rank if mode == "replicas" else 0), d, fri_amd.P)   # replicas: a codeword per rank
         res0 = ctx.commit(coeffs, log_n)
+        exp = _expected(log_n, args.blowup_log) if mode == "single" else None
+        verified = exp is not None and _matches(res0, exp)
+        if exp is not None and not verified:
+            raise SystemExit("1-GPU transcript differs from the C oracle's (tests/golden/bench_transcripts.json)")
+        # inputs resident in HBM: the plan's input buffer, filled by the untimed first commit
+        dptr = ctypes.c_void_p()
+        ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(dptr)))
 
-    # inputs resident in HBM: the plan's input buffer, filled by the untimed first commit
-    dptr = ctypes.c_void_p()
-    ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(dptr)))
-    res = fri_amd.CommitResult()
-    entry = ctx.lib.fri_commit_sharded_device if mode == "sharded" else ctx.lib.fri_commit_device
+        def step():
+            ctx._check(ctx.lib.fri_commit_device(ctx.h, dptr, d, log_n, fri_amd.GENERATOR, None, 0, None,
+                                                 ctypes.byref(res)))
 
-    def step():
-        ctx._check(entry(ctx.h, dptr, d, log_n, fri_amd.GENERATOR, None, 0, None, ctypes.byref(res)))
-
-    def barrier_sync():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
-            torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
+    elapsed = timed(step, args.steps, args.warmup)
     if args.warmup:
         assert _same(res, res0)
-
-    barrier_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     n = 1 << log_n
     ms_per_step = 1000.0 * elapsed / args.steps
     units_per_step = n if mode == "sharded" else world * n
     value = units_per_step * args.steps / elapsed
     blk_log = log_n - (logG if mode == "sharded" else 0)     # layer-0 elements hashed by one GPU
-
     # ---- roofline of the dominant kernel: HIP events on the context stream,
     # recorded around every launch of that kernel during profiled steps.
     roofline = None
@@ -340,9 +415,20 @@ def main():
     if world == 1 and log_n >= 19 and not args.no_extras:
         prover = _prover_stage(ctx, fri_amd, with_cpu=(rank == 0 and not args.no_cpu_baseline))
 
+    # The 1-GPU point of the 2^28 strong-scaling curve (BASELINE configs[4]'s
+    # codeword on one GPU, ~38 GB of HBM), checked against the oracle's
+    # transcript.  Beside `value`, never it.
+    if world == 1 and mode == "single" and log_n < 28 and not args.no_extras:
+        secondary["single_2p28"] = _single_point(fri_amd, device, 28, args.blowup_log, steps=5)
+
+    hbm = ctx.device_bytes()[1]
+    hbm_max = max_over_ranks(float(hbm))
+
     cpu = None
+    configs0 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = _cpu_baseline(coeffs, d, log_n)
+        configs0 = _configs0_stage(ctx)
 
     if rank == 0:
         if mode == "sharded":
@@ -355,15 +441,21 @@ def main():
             workload = (f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} (d=2^{log_n - args.blowup_log}), "
                         f"SHA-256 Merkle per layer, {res.n_rounds} rounds" + (", per GPU" if world > 1 else ""))
             par = f"replicas x{world}" if world > 1 else "single GPU"
+            if fallback:
+                par += f" (FALLBACK: the coset-sharded path failed: {fallback})"
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "field-elems/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 % p coefficients" + (", seed 42)" if mode != "replicas" else ", seed 42+rank)"),
             "config": {"workload": workload, "codeword_log2": log_n, "per_gpu_log2": blk_log,
-                       "blowup": 1 << args.blowup_log, "field": "p=3*2^30+1", "parallelism": par},
+                       "blowup": 1 << args.blowup_log, "field": "p=3*2^30+1", "parallelism": par,
+                       "transport": dist_report},
+            "oracle_verified": bool(verified),
+            "hbm_bytes_per_rank_max": int(hbm_max),
             "roofline": roofline,
             "whole_commit": whole,
+            "scaling_points": secondary or None,
             "breakdown_ms_per_step": breakdown,
             "pcie_inclusive": pcie,
             "decommit": decommit,
@@ -371,9 +463,10 @@ def main():
             "concurrent_commits": concurrent,
             "prover_fibsq": prover,
             "cpu_baseline": cpu,
+            "configs0_cpu": configs0,
         }
-        if note:
-            line["note"] = note
+        if fallback:
+            line["note"] = fallback
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     if mode == "sharded":
         ctx.detach()
@@ -526,10 +619,79 @@ def _pmc_traffic(log_n):
         return None
 
 
+def _single_point(fri_amd, device, log_n, blowup_log, steps):
+    """One more 1-GPU codeword size (its own context), timed over `steps`
+    commits on resident inputs and checked against the oracle transcript."""
+    d = 1 << (log_n - blowup_log)
+    try:
+        cx = fri_amd.Context(device, log_n)
+    except fri_amd.FriError as e:
+        return {"error": str(e)}
+    try:
+        r0 = cx.commit(_coeffs(42, d, fri_amd.P), log_n)
+        exp = _expected(log_n, blowup_log)
+        p = ctypes.c_void_p()
+        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p)))
+        r = fri_amd.CommitResult()
+
+        def st():
+            cx._check(cx.lib.fri_commit_device(cx.h, p, d, log_n, fri_amd.GENERATOR, None, 0, None, ctypes.byref(r)))
+
+        st()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            st()
+        el = time.perf_counter() - t0
+        return {"codeword_log2": log_n, "n_gpus": 1, "ms_per_step": round(1000 * el / steps, 4),
+                "value": round((1 << log_n) * steps / el, 1), "unit": "field-elems/s", "steps": steps,
+                "hbm_bytes": cx.device_bytes()[1],
+                "oracle_verified": exp is not None and _matches(r0, exp) and _same(r, r0)}
+    except fri_amd.FriError as e:
+        return {"error": str(e)}
+    finally:
+        cx.close()
+
+
+def _host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"cpu_model": model, "nproc": avail, "cpu_count": os.cpu_count()}
+
+
+def _median_runs(fn, runs, warmup=1):
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2], ts
+
+
 def _cpu_baseline(coeffs, d, log_n):
-    """Oracle timed on the host (checker only, never the product path):
-    the OpenMP C restatement of the same commit (kind "port") at the full
-    2^log_n workload, plus a single-thread faithful-algorithm sample."""
+    """Oracle timed on the host (checker only, never the product path),
+    following BASELINE.md's CPU-baseline plan:
+      * fast: the OpenMP C restatement (NTT LDE, eval-form fold, SHA-256
+        Merkle, channel) of the same 2^log_n commit on all host threads,
+        median of 5 runs after one warm-up (kind "port": `value`);
+      * faithful: the reference algorithm itself (Horner LDE at every
+        domain point, coefficient fold + Horner re-evaluation; ops.rs:76-83,
+        fri_commit.rs:32-65), one thread like the reference, measured at
+        2^10..2^16 and extrapolated to 2^20 / 2^24 by a least-squares fit
+        t = a*n*d + b*n (labelled extrapolated)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import fri_oracle as fo
@@ -537,36 +699,130 @@ def _cpu_baseline(coeffs, d, log_n):
         lib = fo.load_c_oracle()
     except Exception as e:  # noqa: BLE001
         return {"value": None, "error": f"oracle unavailable: {e}"}
+    host = _host_info()
     c64 = np.ascontiguousarray(coeffs.astype(np.uint64))
     pc = c64.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
-    ch = fo.OrcChannel()
-    lib.orc_channel_init(ctypes.byref(ch))
     r = fo.OrcFriResult()
-    t0 = time.perf_counter()
-    lib.orc_fri_commit_fast(pc, d, log_n, 5, 5, fo.P, ctypes.byref(ch), None, ctypes.byref(r), None, None)
-    t_fast = time.perf_counter() - t0
-    # faithful reference algorithm (Horner LDE, coefficient fold + Horner
-    # re-evaluation), single thread, on a bounded sample codeword 2^13.
-    ls = 13
-    ds = 1 << (ls - 3)
-    cs = np.ascontiguousarray(c64[:ds])
-    pcs = cs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+    def fast():
+        ch = fo.OrcChannel()
+        lib.orc_channel_init(ctypes.byref(ch))
+        lib.orc_fri_commit_fast(pc, d, log_n, 5, 5, fo.P, ctypes.byref(ch), None, ctypes.byref(r), None, None)
+
+    t_fast, runs = _median_runs(fast, 5)
     nthreads = lib.orc_num_threads()
+    exp = _expected(log_n, 3)
+    fast_ok = exp is not None and [bytes(r.roots[k]).hex() for k in range(r.n_layers)] == exp["roots"]
+    # faithful reference algorithm, single thread
     lib.orc_set_num_threads(1)
-    ch2 = fo.OrcChannel()
-    lib.orc_channel_init(ctypes.byref(ch2))
-    t0 = time.perf_counter()
-    lib.orc_fri_commit_faithful(pcs, ds, ls, 5, 5, fo.P, ctypes.byref(ch2), None, ctypes.byref(r), None, None)
-    t_faith = time.perf_counter() - t0
+    pts = []
+    for ls in range(10, 17):
+        ds = 1 << (ls - 3)
+        cs = np.ascontiguousarray(fo.splitmix64_np(42, ds))
+        pcs = cs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+        def faithful():
+            ch2 = fo.OrcChannel()
+            lib.orc_channel_init(ctypes.byref(ch2))
+            lib.orc_fri_commit_faithful(pcs, ds, ls, 5, 5, fo.P, ctypes.byref(ch2), None, ctypes.byref(r), None,
+                                        None)
+
+        t, _ = _median_runs(faithful, 3 if ls <= 14 else 1, warmup=1 if ls <= 14 else 0)
+        pts.append((ls, ds, t))
     lib.orc_set_num_threads(nthreads)
+    A = np.array([[(1 << ls) * ds, 1 << ls] for ls, ds, _ in pts], dtype=np.float64)
+    y = np.array([t for _, _, t in pts])
+    w = 1.0 / y                                       # relative least squares
+    (a, b), *_ = np.linalg.lstsq(A * w[:, None], y * w, rcond=None)
+
+    def extrap(L):
+        n_, d_ = 1 << L, 1 << (L - 3)
+        t = a * n_ * d_ + b * n_
+        return {"codeword_log2": L, "seconds": float(f"{t:.4g}"), "value": round(n_ / t, 1), "extrapolated": True}
+
     return {"value": round((1 << log_n) / t_fast, 1), "unit": "field-elems/s", "cores": nthreads,
-            "kind": "port",
+            "kind": "port", "host": host, "oracle_verified": fast_ok,
             "sample": f"full workload: OpenMP C restatement (NTT LDE, eval-form fold, SHA-256 Merkle, channel) "
-                      f"at codeword 2^{log_n}, one commit, {t_fast:.2f} s",
-            "faithful_sample": {"value": round((1 << ls) / t_faith, 1), "unit": "field-elems/s", "cores": 1,
-                                "sample": f"reference algorithm (Horner LDE + coefficient fold + Horner "
-                                          f"re-evaluation) at codeword 2^{ls}, d=2^{ls - 3}, {t_faith:.2f} s; "
-                                          f"O(n*d) so 2^24 would be ~{(2**24/2**ls)**2 * t_faith / 86400:.0f} days"}}
+                      f"at codeword 2^{log_n}, median of 5 runs after 1 warm-up: {t_fast:.3f} s "
+                      f"(runs {', '.join(f'{t:.3f}' for t in runs)})",
+            "faithful": {"kind": "port", "cores": 1,
+                         "what": "reference algorithm (Horner LDE + coefficient fold + Horner re-evaluation, "
+                                 "SHA-256 rs_merkle tree, hex channel), one thread",
+                         "measured": [{"codeword_log2": ls, "d": ds, "seconds": round(t, 5),
+                                       "value": round((1 << ls) / t, 1)} for ls, ds, t in pts],
+                         "fit": {"model": "t = a*n*d + b*n", "a_ns_per_horner_step": round(a * 1e9, 4),
+                                 "b_ns_per_element": round(b * 1e9, 2)},
+                         "at_2p20": extrap(20), "at_2p24": extrap(24)}}
+
+
+def _configs0_stage(ctx):
+    """BASELINE configs[0] (benches/poly_ops.rs / poly_lang.rs shape, CPU-only
+    in the reference): the reference's two LDE/interpolation primitives at the
+    published sizes, restated in the C oracle over p = 3*2^30+1 (one thread),
+    printed beside the reference's own criterion numbers (macOS laptop,
+    moduli 17 / 7), plus this repo's NTT / iNTT at degree 2^10 on
+    the host (oracle) and through the GPU library (host buffers in and out)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import fri_oracle as fo
+    lib = fo.load_c_oracle()
+    nth = lib.orc_num_threads()
+    lib.orc_set_num_threads(1)
+    P = fo.P
+    p64 = ctypes.POINTER(ctypes.c_uint64)
+
+    def per_call(fn, target_s=0.2):
+        k = 1
+        while True:
+            t0 = time.perf_counter()
+            for _ in range(k):
+                fn()
+            t = time.perf_counter() - t0
+            if t >= target_s or k >= 1 << 20:
+                return t / k
+            k *= 4
+
+    out = {"reference_published": {
+        "Eval_17_ns": {"10": 33.752, "100": 603.66, "1000": 6488.7, "5000": 32277.0},
+        "interpolate_lagrange_us": {"10": 28.956, "50": 95.849, "100": 215.36, "200": 526.25, "500": 2383.3},
+        "source": "criterion screenshots, macOS laptop (results/12:08/..., results/base/langrange_bench.png); "
+                  "benches/poly_ops.rs:161-181, benches/poly_lang.rs:33-51; moduli 17 and 7"}}
+    ev = {}
+    for deg in (10, 100, 1000, 5000):
+        c = np.ascontiguousarray(fo.splitmix64_np(3333, deg + 1))
+        x = int(fo.splitmix64_np(7, 1)[0])
+        ev[str(deg)] = round(1e9 * per_call(lambda: lib.orc_poly_evaluate(c.ctypes.data_as(p64), deg + 1, x, P)), 1)
+    out["evaluate_horner_ns"] = ev
+    lg = {}
+    for n in (10, 50, 100, 200, 500):
+        xs = np.ascontiguousarray(fo.splitmix64_np(11, n))
+        ys = np.ascontiguousarray(fo.splitmix64_np(12, n))
+        o = np.zeros(n + 1, dtype=np.uint64)
+        lg[str(n)] = round(1e6 * per_call(lambda: lib.orc_interpolate_lagrange(
+            xs.ctypes.data_as(p64), ys.ctypes.data_as(p64), n, o.ctypes.data_as(p64), P)), 2)
+    out["interpolate_lagrange_us"] = lg
+    # degree 2^10: NTT LDE (blowup 8) and coset iNTT interpolate
+    c = np.ascontiguousarray(fo.splitmix64_np(42, 1 << 10))
+    ev_out = np.zeros(1 << 13, dtype=np.uint64)
+    ys = np.ascontiguousarray(fo.splitmix64_np(43, 1 << 10))
+    co = np.zeros(1 << 10, dtype=np.uint64)
+    out["ntt_lde_2p10_to_2p13_us"] = round(1e6 * per_call(lambda: lib.orc_lde(
+        c.ctypes.data_as(p64), 1 << 10, 13, 5, 5, P, ev_out.ctypes.data_as(p64))), 2)
+    out["intt_interpolate_2p10_us"] = round(1e6 * per_call(lambda: lib.orc_interpolate_coset(
+        ys.ctypes.data_as(p64), 10, 5, 5, P, co.ctypes.data_as(p64))), 2)
+    lib.orc_set_num_threads(nth)
+    c32, y32 = c.astype(np.uint32), ys.astype(np.uint32)
+    gl = ctx.lde(c32, 13)
+    gi = ctx.interpolate(y32)
+    out["gpu_matches_oracle"] = bool(np.array_equal(gl, ev_out.astype(np.uint32))
+                                     and np.array_equal(gi, co[:gi.size].astype(np.uint32)))
+    out["gpu_lde_2p10_to_2p13_us"] = round(1e6 * per_call(lambda: ctx.lde(c32, 13)), 2)
+    out["gpu_interpolate_2p10_us"] = round(1e6 * per_call(lambda: ctx.interpolate(y32)), 2)
+    out["host"] = _host_info()
+    out["what"] = ("C oracle over p=3*2^30+1, one thread: Horner evaluate (ops.rs:76-83) at the Eval_17 degrees, "
+                   "Lagrange interpolate (interpolation.rs:121-152) at the poly_lang sizes, NTT LDE / iNTT at "
+                   "degree 2^10; GPU: fri_lde / fri_interpolate with host buffers (launch + copies dominate)")
+    return out
 
 
 if __name__ == "__main__":

@@ -259,6 +259,13 @@ int fri_dist_attach_rccl(fri_ctx* ctx, int rank, int world, const uint8_t uid[12
 /* Host-callback transport (e.g. torch.distributed gloo; used by tests). */
 int fri_dist_attach_host(fri_ctx* ctx, int rank, int world, const fri_collectives* ops);
 int fri_dist_detach(fri_ctx* ctx);
+/* The attached transport: FRI_TRANSPORT_NONE / _RCCL / _HOST, and for RCCL
+ * the rank and world size the communicator itself reports
+ * (ncclCommUserRank / ncclCommCount). */
+#define FRI_TRANSPORT_NONE 0
+#define FRI_TRANSPORT_RCCL 1
+#define FRI_TRANSPORT_HOST 2
+int fri_dist_info(fri_ctx* ctx, int* rank, int* world, int* transport);
 /* Diagnostic: run the transport's all-to-all, all-gather and pair exchange
  * (both streams) on a known pattern and check the result; FRI_ERCCL with a
  * message on mismatch.  Collective: every rank must call it.  world == 1
@@ -267,6 +274,10 @@ int fri_dist_selftest(fri_ctx* ctx, size_t words_per_peer);
 
 /* Sharded fri_commit: every rank passes the same full coefficient vector and
  * channel state and gets the same result.  world == 1 is fri_commit.
+ * Each rank's plan is shard-sized: it allocates only its block of every
+ * sharded layer and tree and the x^-1 slices its folds read (plus the full
+ * coefficient vector and the < 2^20 local tail), so a context created with
+ * log_n_max = log_n - log2(world) suffices (2^28 over 8 ranks: ~6 GiB each).
  * Afterwards fri_layer_copy / fri_tree_level_copy / fri_auth_path serve the
  * layers finished on every rank (the < 2^20 tail); the sharded layers return
  * FRI_ESTATE (each rank holds only its block). */
@@ -288,10 +299,20 @@ int fri_set_profiling(fri_ctx* ctx, int enabled);
 int fri_get_profile(fri_ctx* ctx, const char* kernel_class, double* total_ms, uint64_t* launches,
                     uint64_t* bytes);
 int fri_reset_profile(fri_ctx* ctx);
+/* Device memory (HBM) the context holds now and at most so far, in bytes:
+ * twiddles, scratch, the commit plan (layers, trees, x^-1 tables), multi-GPU
+ * buffers and any grown scratch.  (Diagnostic; no reference counterpart.) */
+int fri_ctx_device_bytes(fri_ctx* ctx, uint64_t* current, uint64_t* peak);
 /* Diagnostic build only (-DFRI_STAMPS): top-kernel phase timestamps of the
  * last commit, (FRI_MAX_LAYERS x 24) u64 ticks of the 100 MHz clock.
  * Returns FRI_ESTATE in the product build. */
 int fri_debug_stamps(fri_ctx* ctx, uint64_t* out, size_t cap);
+/* Test hook for the collective deadline (fri_dist_attach_rccl): with enable
+ * != 0 the next RCCL all-to-all on the context is replaced by a kernel that
+ * waits like a collective whose peer never arrives, until the deadline's
+ * abort releases it.  The call then returns FRI_ERCCL and later sharded calls
+ * FRI_ESTATE, exactly as for a real stall. */
+int fri_debug_inject_stall(fri_ctx* ctx, int enable);
 
 #ifdef __cplusplus
 }

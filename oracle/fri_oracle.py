@@ -524,6 +524,19 @@ def splitmix64_field(seed: int, count: int, M: int = P) -> List[int]:
     return out
 
 
+def splitmix64_np(seed: int, count: int, M: int = P):
+    """splitmix64_field as a numpy uint64 array (the same stream, vectorised;
+    tests check the two agree) for the large configs, 2^25 coefficients."""
+    import numpy as np
+    idx = np.arange(1, count + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed & ((1 << 64) - 1)) + idx * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z % np.uint64(M)
+
+
 # --------------------------------------------------------------------------
 # ctypes loader for the C oracle (oracle/fri_oracle.c -> oracle/_build/liboracle.so)
 # --------------------------------------------------------------------------

@@ -33,12 +33,20 @@ struct Plan {
     size_t d = 0;
     uint32_t offset = 0;
     int rmax = 0;
+    // Shard-sized plan (fri_commit_sharded): rank `rank` of G holds only its
+    // block of layers 0..k_sw (their slots, block-local trees and x^-1 slices
+    // are block-sized); layers after k_sw are full-size local layers, and
+    // layer k_sw's value slot is full-size when the tail goes local.
+    bool sharded = false;
+    uint32_t G = 1, rank = 0;
+    int k_sw = -1;
     uint32_t* d_in = nullptr;   size_t in_cap = 0;
     uint32_t* coefA = nullptr;
     uint32_t* coefB = nullptr;  size_t coef_cap = 0;
     uint32_t* layers = nullptr; size_t layer_off[MAXR + 2] = {0};
     uint32_t* trees = nullptr;  size_t tree_off[MAXR + 2] = {0};
     uint32_t* xinv = nullptr;   size_t xinv_off[MAXR + 2] = {0};
+    size_t xinv_start[MAXR + 2] = {0};   // domain index of xinv slot k's first entry (sharded slices)
     uint32_t* pre_lo = nullptr;
     uint32_t* pre_hi = nullptr;
     int32_t* wgmax = nullptr;       // per-workgroup coefficient maxima
@@ -117,7 +125,35 @@ struct fri_ctx {
     size_t trace_tree_cap = 0;      // leaves they can hold
     bool trace_valid = false;       // a trace commit is resident
     uint32_t trace_log_t = 0, trace_log_b = 0, trace_offset = 0;
+    bool inject_stall = false;        // fri_debug_inject_stall: next RCCL all-to-all never completes
+    uint32_t* stall_flag = nullptr;   // pinned host word the stalled kernel polls (set by rccl_abort)
+    uint32_t* stall_flag_dev = nullptr;
+    std::map<const void*, size_t> allocs;   // device allocations owned by the context (fri_ctx_device_bytes)
+    size_t dev_bytes = 0, dev_peak = 0;
 };
+
+// Device allocations of a context go through these, so that
+// fri_ctx_device_bytes can report what one rank / one context holds in HBM.
+template <class T>
+static hipError_t dalloc(fri_ctx* ctx, T** p, size_t bytes) {
+    void* q = nullptr;
+    const hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) { *p = nullptr; return e; }
+    *p = static_cast<T*>(q);
+    ctx->allocs[q] = bytes;
+    ctx->dev_bytes += bytes;
+    if (ctx->dev_bytes > ctx->dev_peak) ctx->dev_peak = ctx->dev_bytes;
+    return hipSuccess;
+}
+static void dfree(fri_ctx* ctx, const void* p) {
+    if (!p) return;
+    auto it = ctx->allocs.find(p);
+    if (it != ctx->allocs.end()) {
+        ctx->dev_bytes -= it->second;
+        ctx->allocs.erase(it);
+    }
+    hipFree(const_cast<void*>(p));
+}
 
 #define FRI_HIP(ctx, expr)                                                              \
     do {                                                                                \
@@ -200,14 +236,14 @@ extern "C" int fri_ctx_create(int device, uint32_t log_n_max, fri_ctx** out) {
     if ((expr) != hipSuccess) { fri_ctx_destroy(ctx); return FRI_ENOMEM; }
     CK(hipSetDevice(device));
     CK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    CK(hipMalloc(&ctx->tw_fwd, N * 4));
-    CK(hipMalloc(&ctx->tw_inv, N * 4));
-    CK(hipMalloc(&ctx->scratch_a, N * 4));
-    CK(hipMalloc(&ctx->scratch_b, N * 4));
-    CK(hipMalloc(&ctx->scratch_c, N * 4));
-    CK(hipMalloc(&ctx->pow_lo, ((size_t)1 << POW_LO_LOG) * 4));
-    CK(hipMalloc(&ctx->pow_hi, nhi * 4));
-    CK(hipMalloc(&ctx->d_state, sizeof(DevState)));
+    CK(dalloc(ctx, &ctx->tw_fwd, N * 4));
+    CK(dalloc(ctx, &ctx->tw_inv, N * 4));
+    CK(dalloc(ctx, &ctx->scratch_a, N * 4));
+    CK(dalloc(ctx, &ctx->scratch_b, N * 4));
+    CK(dalloc(ctx, &ctx->scratch_c, N * 4));
+    CK(dalloc(ctx, &ctx->pow_lo, ((size_t)1 << POW_LO_LOG) * 4));
+    CK(dalloc(ctx, &ctx->pow_hi, nhi * 4));
+    CK(dalloc(ctx, &ctx->d_state, sizeof(DevState)));
     CK(hipHostMalloc(&ctx->h_state, sizeof(DevState), hipHostMallocDefault));
 #undef CK
     launch_twiddles(ctx->tw_fwd, log_n_max, false, ctx->stream);
@@ -223,8 +259,8 @@ static void plan_free(fri_ctx* ctx) {
     Plan& p = ctx->plan;
     if (p.exec) hipGraphExecDestroy(p.exec);
     if (p.graph) hipGraphDestroy(p.graph);
-    hipFree(p.d_in); hipFree(p.coefA); hipFree(p.coefB); hipFree(p.layers);
-    hipFree(p.trees); hipFree(p.xinv); hipFree(p.pre_lo); hipFree(p.pre_hi); hipFree(p.wgmax);
+    dfree(ctx, p.d_in); dfree(ctx, p.coefA); dfree(ctx, p.coefB); dfree(ctx, p.layers);
+    dfree(ctx, p.trees); dfree(ctx, p.xinv); dfree(ctx, p.pre_lo); dfree(ctx, p.pre_hi); dfree(ctx, p.wgmax);
     p = Plan();
 }
 
@@ -235,22 +271,23 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     plan_free(ctx);
     for (auto e : ctx->event_pool) hipEventDestroy(e);
     fri_dist_detach(ctx);
-    hipFree(ctx->db.cyc); hipFree(ctx->db.recv); hipFree(ctx->db.half); hipFree(ctx->db.roots);
-    hipFree(ctx->db.top); hipFree(ctx->db.pre_lo); hipFree(ctx->db.pre_hi); hipFree(ctx->db.gath);
+    dfree(ctx, ctx->db.cyc); dfree(ctx, ctx->db.recv); dfree(ctx, ctx->db.half); dfree(ctx, ctx->db.roots);
+    dfree(ctx, ctx->db.top); dfree(ctx, ctx->db.pre_lo); dfree(ctx, ctx->db.pre_hi); dfree(ctx, ctx->db.gath);
     if (ctx->xstream) hipStreamDestroy(ctx->xstream);
     if (ctx->ev_vals) hipEventDestroy(ctx->ev_vals);
     if (ctx->ev_xchg) hipEventDestroy(ctx->ev_xchg);
     if (ctx->cstream) hipStreamDestroy(ctx->cstream);
     if (ctx->ev_pre) hipEventDestroy(ctx->ev_pre);
     if (ctx->ev_coef) hipEventDestroy(ctx->ev_coef);
-    hipFree(ctx->tw_fwd); hipFree(ctx->tw_inv);
-    hipFree(ctx->scratch_a); hipFree(ctx->scratch_b); hipFree(ctx->scratch_c);
-    hipFree(ctx->pow_lo); hipFree(ctx->pow_hi);
-    hipFree(ctx->d_state);
+    dfree(ctx, ctx->tw_fwd); dfree(ctx, ctx->tw_inv);
+    dfree(ctx, ctx->scratch_a); dfree(ctx, ctx->scratch_b); dfree(ctx, ctx->scratch_c);
+    dfree(ctx, ctx->pow_lo); dfree(ctx, ctx->pow_hi);
+    dfree(ctx, ctx->d_state);
     if (ctx->dq_host) hipHostFree(ctx->dq_host);
-    if (ctx->interp_tmp) hipFree(ctx->interp_tmp);
-    hipFree(ctx->trace_tree);
-    hipFree(ctx->trace_lde);
+    if (ctx->stall_flag) hipHostFree(ctx->stall_flag);
+    if (ctx->interp_tmp) dfree(ctx, ctx->interp_tmp);
+    dfree(ctx, ctx->trace_tree);
+    dfree(ctx, ctx->trace_lde);
     if (ctx->h_state) hipHostFree(ctx->h_state);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -336,12 +373,24 @@ extern "C" int fri_interpolate(fri_ctx* ctx, const uint32_t* ys, uint32_t log_n,
 static int ensure_tmp(fri_ctx* ctx, size_t words) {
     if (words <= ctx->interp_cap) return FRI_OK;
     FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->interp_tmp) hipFree(ctx->interp_tmp);
+    if (ctx->interp_tmp) dfree(ctx, ctx->interp_tmp);
     ctx->interp_tmp = nullptr;
     ctx->interp_cap = 0;
-    if (hipMalloc(&ctx->interp_tmp, words * 4) != hipSuccess) return fail(ctx, FRI_ENOMEM, "partials scratch");
+    if (dalloc(ctx, &ctx->interp_tmp, words * 4) != hipSuccess) return fail(ctx, FRI_ENOMEM, "partials scratch");
     ctx->interp_cap = words;
     return FRI_OK;
+}
+// Scratch grown past TMP_KEEP_WORDS is released after the call that grew it,
+// so one large fri_merkle_root (the tree of 2^28 values is 16 GiB) does not
+// pin HBM for the life of the context and starve a later commit plan; smaller
+// scratch is kept (no hipFree, which synchronises the device, per call).
+constexpr size_t TMP_KEEP_WORDS = (size_t)1 << 26;   // 256 MiB
+static void tmp_trim(fri_ctx* ctx) {
+    if (ctx->interp_cap <= TMP_KEEP_WORDS) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    dfree(ctx, ctx->interp_tmp);
+    ctx->interp_tmp = nullptr;
+    ctx->interp_cap = 0;
 }
 
 // interpolate_lagrange_polynomials (interpolation.rs:121-152) on arbitrary
@@ -378,6 +427,7 @@ extern "C" int fri_interpolate_points(fri_ctx* ctx, const uint32_t* xs, const ui
     FRI_HIP(ctx, hipGetLastError());
     FRI_HIP(ctx, hipMemcpyAsync(coeffs_out, ctx->scratch_a, n * 4, hipMemcpyDeviceToHost, s));   // deg f < n
     FRI_HIP(ctx, hipStreamSynchronize(s));
+    tmp_trim(ctx);
     size_t len = n;
     while (len > 0 && coeffs_out[len - 1] == 0) len--;          // Polynomial::new trim (ops.rs:19-37)
     *len_out = len;
@@ -403,6 +453,7 @@ extern "C" int fri_evaluate(fri_ctx* ctx, const uint32_t* coeffs, size_t d, cons
     FRI_HIP(ctx, hipGetLastError());
     if (count) FRI_HIP(ctx, hipMemcpyAsync(out, ctx->scratch_c, count * 4, hipMemcpyDeviceToHost, ctx->stream));
     FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    tmp_trim(ctx);
     return FRI_OK;
 }
 
@@ -462,13 +513,13 @@ extern "C" int fri_trace_commit(fri_ctx* ctx, const uint32_t* trace, uint32_t lo
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     ctx->trace_valid = false;
     if (ctx->trace_tree_cap < n) {
-        hipFree(ctx->trace_tree);
-        hipFree(ctx->trace_lde);
+        dfree(ctx, ctx->trace_tree);
+        dfree(ctx, ctx->trace_lde);
         ctx->trace_tree = nullptr;
         ctx->trace_lde = nullptr;
         ctx->trace_tree_cap = 0;
-        FRI_HIP(ctx, hipMalloc(&ctx->trace_tree, (n * 2) * 32));
-        FRI_HIP(ctx, hipMalloc(&ctx->trace_lde, n * 4));
+        FRI_HIP(ctx, dalloc(ctx, &ctx->trace_tree, (n * 2) * 32));
+        FRI_HIP(ctx, dalloc(ctx, &ctx->trace_lde, n * 4));
         ctx->trace_tree_cap = n;
     }
     hipStream_t s = ctx->stream;
@@ -562,6 +613,7 @@ extern "C" int fri_merkle_root(fri_ctx* ctx, const uint32_t* values, size_t n, u
     uint32_t w[8];
     hipError_t e1 = hipMemcpyAsync(w, root_dev, 32, hipMemcpyDeviceToHost, ctx->stream);
     hipError_t e2 = hipStreamSynchronize(ctx->stream);
+    tmp_trim(ctx);
     FRI_HIP(ctx, e1);
     FRI_HIP(ctx, e2);
     digest_to_bytes(w, root32);
@@ -576,42 +628,113 @@ static int rounds_bound(size_t d, uint32_t log_n) {
     return b < (int)log_n ? b : (int)log_n;
 }
 
-static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset) {
+// ---- coset-sharded schedule (shared by the shard-sized plan and the commit) --
+constexpr uint32_t SHARD_MIN_LOG = 20;   // layers of >= 2^20 elements are hashed sharded
+
+// Layer k of a sharded commit hands a sharded layer k+1 on while that layer
+// is still large (>= 2^SHARD_MIN_LOG) and its blocks hold >= 2^10 elements;
+// otherwise layer k is the last sharded one (k_sw) and the tail goes local.
+static bool next_layer_sharded(uint32_t log_n, uint32_t logG, int k, int rmax) {
+    const uint32_t Lk = log_n - (uint32_t)k;
+    return k < rmax && (Lk - 1) >= SHARD_MIN_LOG && (Lk - 1 - logG) >= 10;
+}
+static int switch_layer(uint32_t log_n, uint32_t logG, int rmax) {
+    int k = 0;
+    while (next_layer_sharded(log_n, logG, k, rmax)) k++;
+    return k;
+}
+// The fold pairs block b with block b + G/2 (fold pairs (i, i + m/2)); the
+// rank holding b (< G/2) keeps output block 2b, its partner 2b + 1.
+static void advance_blocks(std::vector<uint32_t>& block_of, std::vector<uint32_t>& rank_of, uint32_t G) {
+    for (uint32_t r = 0; r < G; r++) {
+        const uint32_t br = block_of[r];
+        block_of[r] = br < G / 2 ? 2 * br : 2 * (br - G / 2) + 1;
+    }
+    for (uint32_t r = 0; r < G; r++) rank_of[block_of[r]] = r;
+}
+// Domain index of the first x^-1 a sharded fold of layer k needs on a rank
+// holding block b of size B: the half-block [bb*B + (isA ? 0 : B/2), + B/2).
+static size_t fold_xinv_start(uint32_t b, uint32_t G, size_t B) {
+    const bool isA = b < G / 2;
+    return (size_t)(isA ? b : b - G / 2) * B + (isA ? 0 : B / 2);
+}
+
+// G == 1: the whole-codeword plan of fri_commit.  G > 1: the shard-sized plan
+// of rank `rank` (see Plan::sharded); its x^-1 slots hold only the slices the
+// rank's folds read, computed directly as (offset^(2^k) w_{n_k}^i)^-1 (the
+// same values the whole-domain squaring chain gives: D_k = D_0^(2^k)).
+static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, uint32_t G = 1, uint32_t rank = 0) {
     Plan& p = ctx->plan;
-    if (p.valid && p.d == d && p.log_n == log_n && p.offset == offset) return FRI_OK;
+    const bool sharded = G > 1;
+    if (p.valid && p.d == d && p.log_n == log_n && p.offset == offset && p.sharded == sharded && p.G == G &&
+        p.rank == rank)
+        return FRI_OK;
     plan_free(ctx);
     const size_t n = (size_t)1 << log_n;
+    uint32_t logG = 0;
+    while ((1u << logG) < G) logG++;
     p.log_n = log_n;
     p.d = d;
     p.offset = offset;
     p.rmax = rounds_bound(d, log_n);
+    p.sharded = sharded;
+    p.G = G;
+    p.rank = rank;
+    p.k_sw = sharded ? switch_layer(log_n, logG, p.rmax) : -1;
+    const bool local_tail = sharded && p.k_sw < p.rmax;
+    std::vector<uint32_t> block_of(G), rank_of(G);
+    for (uint32_t r = 0; r < G; r++) block_of[r] = rank_of[r] = r;
     size_t lay = 0, tre = 0, xin = 0;
     for (int k = 0; k <= p.rmax; k++) {
-        uint32_t L = log_n - (uint32_t)k;
+        const uint32_t L = log_n - (uint32_t)k;
+        const bool blk = sharded && k <= p.k_sw;               // block-local tree
+        const uint32_t Lt = blk ? L - logG : L;
         p.layer_off[k] = lay;
         p.tree_off[k] = tre;
         p.xinv_off[k] = xin;
-        lay += (size_t)1 << L;
-        tre += 8 * (((size_t)2 << L) - 1);
-        if (k < p.rmax) xin += ((size_t)1 << L) / 2;
+        p.xinv_start[k] = 0;
+        lay += (blk && !(k == p.k_sw && local_tail)) ? ((size_t)1 << Lt) : ((size_t)1 << L);
+        tre += 8 * (((size_t)2 << Lt) - 1);
+        if (k < p.rmax) {
+            if (sharded && k < p.k_sw) {                        // sharded fold: this rank's half-block slice
+                const size_t B = (size_t)1 << Lt;
+                p.xinv_start[k] = fold_xinv_start(block_of[rank], G, B);
+                xin += B / 2;
+                advance_blocks(block_of, rank_of, G);
+            } else {
+                xin += ((size_t)1 << L) / 2;
+            }
+        }
     }
     p.layer_off[p.rmax + 1] = lay;
     p.tree_off[p.rmax + 1] = tre;
     p.in_cap = d ? d : 1;
     p.coef_cap = d / 2 + 1;
     const size_t nhi = log_n > POW_LO_LOG ? ((size_t)1 << (log_n - POW_LO_LOG)) : 1;
-    if (hipMalloc(&p.d_in, p.in_cap * 4) != hipSuccess || hipMalloc(&p.coefA, p.coef_cap * 4) != hipSuccess ||
-        hipMalloc(&p.coefB, p.coef_cap * 4) != hipSuccess || hipMalloc(&p.layers, lay * 4) != hipSuccess ||
-        hipMalloc(&p.trees, tre * 4) != hipSuccess || hipMalloc(&p.xinv, (xin ? xin : 1) * 4) != hipSuccess ||
-        hipMalloc(&p.pre_lo, ((size_t)1 << POW_LO_LOG) * 4) != hipSuccess ||
-        hipMalloc(&p.pre_hi, nhi * 4) != hipSuccess ||
-        hipMalloc(&p.wgmax, 6 * ((log_n > 8 ? ((size_t)1 << (log_n - 8)) : 1) + 16) * 4) != hipSuccess) {
+    if (dalloc(ctx, &p.d_in, p.in_cap * 4) != hipSuccess || dalloc(ctx, &p.coefA, p.coef_cap * 4) != hipSuccess ||
+        dalloc(ctx, &p.coefB, p.coef_cap * 4) != hipSuccess || dalloc(ctx, &p.layers, lay * 4) != hipSuccess ||
+        dalloc(ctx, &p.trees, tre * 4) != hipSuccess || dalloc(ctx, &p.xinv, (xin ? xin : 1) * 4) != hipSuccess ||
+        dalloc(ctx, &p.pre_lo, ((size_t)1 << POW_LO_LOG) * 4) != hipSuccess ||
+        dalloc(ctx, &p.pre_hi, nhi * 4) != hipSuccess ||
+        dalloc(ctx, &p.wgmax, 6 * ((log_n > 8 ? ((size_t)1 << (log_n - 8)) : 1) + 16) * 4) != hipSuccess) {
         plan_free(ctx);
         return fail(ctx, FRI_ENOMEM, "device allocation failed for commit plan");
     }
     hipStream_t s = ctx->stream;
     launch_pow_table(p.pre_lo, p.pre_hi, log_n, offset, 1u, s);
-    if (p.rmax > 0) {
+    if (sharded) {
+        // every slot from its own points; the layer buffer (rewritten by every
+        // commit, and at least as large as any slot) holds the points
+        uint32_t offk = offset;                               // offset^(2^k)
+        for (int k = 0; k < p.rmax; k++) {
+            const uint32_t L = log_n - (uint32_t)k;
+            const size_t cnt = p.xinv_off[k + 1] - p.xinv_off[k];
+            const uint32_t first = mul_std(offk, pow_std(root_of_unity(L), (uint64_t)p.xinv_start[k]));
+            launch_coset_points(p.layers, cnt, first, L, s);
+            launch_batch_inverse(p.layers, p.xinv + p.xinv_off[k], cnt, 1, s);
+            offk = mul_std(offk, offk);
+        }
+    } else if (p.rmax > 0) {
         // Domain inverses for every fold, built with the batch-inverse kernel:
         // xinv_0[i] = (offset*w_n^i)^-1, xinv_k[i] = xinv_{k-1}[i]^2 (D_k = D_{k-1}^2).
         launch_coset_points(ctx->scratch_a, n / 2, offset, log_n, s);
@@ -851,6 +974,12 @@ extern "C" int fri_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level,
     return FRI_OK;
 }
 
+// One query's value and path through the decommitment gather kernel (a
+// one-layer DecommitPlan): one launch that writes the big-endian path
+// straight into the pinned host buffer, instead of one blocking copy per
+// tree level.
+static int dq_alloc(fri_ctx* ctx);
+
 extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint32_t* value_out, uint8_t* path,
                              uint32_t* depth_out) {
     if (!ctx || !value_out || !depth_out) return fail(ctx, FRI_EINVAL, "null argument");
@@ -860,14 +989,20 @@ extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint3
         return fail(ctx, FRI_ESTATE, "layer was committed sharded: this rank holds only its block (fri_commit_sharded)");
     uint32_t L = p.log_n - layer;
     if (index >> L) return fail(ctx, FRI_EINVAL, "index out of range");
-    FRI_HIP(ctx, hipMemcpy(value_out, p.layers + p.layer_off[layer] + index, 4, hipMemcpyDeviceToHost));
-    for (uint32_t l = 0; l < L && path; l++) {
-        uint64_t sib = (index >> l) ^ 1u;
-        uint32_t w[8];
-        FRI_HIP(ctx, hipMemcpy(w, p.trees + p.tree_off[layer] + 8 * (level_offset(L, l) + sib), 32,
-                               hipMemcpyDeviceToHost));
-        digest_to_bytes(w, path + 32 * l);
-    }
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = dq_alloc(ctx);
+    if (rc) return rc;
+    DecommitPlan dp{};
+    dp.index = index;
+    dp.log_n = L;
+    dp.n_layers = 1;
+    dp.layer_off[0] = p.layer_off[layer];
+    dp.tree_off[0] = p.tree_off[layer];
+    launch_decommit_gather(p.layers, p.trees, dp, ctx->dq_dev, ctx->stream);
+    FRI_HIP(ctx, hipGetLastError());
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *value_out = ctx->dq_host[0];
+    if (path) memcpy(path, ctx->dq_host + 2, (size_t)32 * L);     // [value, sibling value, path(index), ...]
     *depth_out = L;
     return FRI_OK;
 }
@@ -1061,6 +1196,24 @@ extern "C" int fri_reset_profile(fri_ctx* ctx) {
     ctx->prof.clear();
     return FRI_OK;
 }
+extern "C" int fri_debug_inject_stall(fri_ctx* ctx, int enable) {
+    if (!ctx) return FRI_EINVAL;
+    if (!ctx->stall_flag) {
+        FRI_HIP(ctx, hipHostMalloc(&ctx->stall_flag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        void* d = nullptr;
+        FRI_HIP(ctx, hipHostGetDevicePointer(&d, ctx->stall_flag, 0));
+        ctx->stall_flag_dev = static_cast<uint32_t*>(d);
+        *ctx->stall_flag = 1u;
+    }
+    ctx->inject_stall = enable != 0;
+    return FRI_OK;
+}
+extern "C" int fri_ctx_device_bytes(fri_ctx* ctx, uint64_t* current, uint64_t* peak) {
+    if (!ctx || !current || !peak) return fail(ctx, FRI_EINVAL, "null argument");
+    *current = ctx->dev_bytes;
+    *peak = ctx->dev_peak;
+    return FRI_OK;
+}
 
 // =================================================================== multi-GPU
 static int tp_host_stage(fri_ctx* ctx, size_t bytes) {
@@ -1091,11 +1244,22 @@ static double rccl_timeout_s() {
 static double seconds_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
+// Test hook (fri_debug_inject_stall): the next RCCL all-to-all is replaced by
+// a one-lane kernel that waits, like an RCCL kernel whose peer never comes,
+// until the abort releases it (or, as a bound every wave reaches, 60 s pass).
+__global__ void k_stalled_collective(const uint32_t* flag, uint64_t max_ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u &&
+           wall_clock64() - t0 < max_ticks)
+        __builtin_amdgcn_s_sleep(127);
+}
+
 static void rccl_abort(fri_ctx* ctx) {
     Transport& tp = ctx->tp;
     if (tp.xcomm) ncclCommAbort(tp.xcomm);
     if (tp.comm) ncclCommAbort(tp.comm);
     tp.comm = tp.xcomm = nullptr;      // the transport is gone: later sharded calls see FRI_ESTATE
+    if (ctx->stall_flag) __atomic_store_n(ctx->stall_flag, 1u, __ATOMIC_SEQ_CST);   // ends an injected stall
 }
 #define FRI_NCCL(ctx, expr)                                                                  \
     do {                                                                                     \
@@ -1112,18 +1276,29 @@ static int sync_sharded(fri_ctx* ctx, hipStream_t s) {
     }
     const auto t0 = std::chrono::steady_clock::now();
     const double lim = rccl_timeout_s();
+    // spin (yielding) for the first 200 us, which covers a commit's short
+    // syncs at full responsiveness, then poll every 50 us so that a rank
+    // waiting on its peers does not hold a host core at 100%
     for (;;) {
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) return FRI_OK;
         if (e != hipErrorNotReady) FRI_HIP(ctx, e);
-        if (seconds_since(t0) > lim) {
-            rccl_abort(ctx);
-            (void)hipStreamSynchronize(s);
-            return fail(ctx, FRI_ERCCL, "sharded commit: no progress in " + std::to_string((int)lim) +
-                                            " s (RCCL communicators aborted)");
-        }
-        std::this_thread::yield();
+        const double el = seconds_since(t0);
+        if (el > lim) break;
+        if (el < 2e-4) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
+    rccl_abort(ctx);
+    // the abort ends RCCL kernels spinning on an absent peer; the wait for
+    // the stream to drain is bounded as well (a stream still busy after it
+    // is reported, and the context must then not be reused for commits)
+    const auto t1 = std::chrono::steady_clock::now();
+    bool drained = false;
+    while (!(drained = hipStreamQuery(s) != hipErrorNotReady) && seconds_since(t1) < lim)
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    return fail(ctx, FRI_ERCCL, "sharded commit: no progress in " + std::to_string((int)lim) +
+                                    " s (RCCL communicators aborted" +
+                                    (drained ? ")" : "; stream still busy: destroy the context)"));
 }
 
 static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
@@ -1143,6 +1318,14 @@ static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t byt
 
 static int tp_alltoall(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes_per_peer, hipStream_t s) {
     Transport& tp = ctx->tp;
+    if (!tp.host && ctx->inject_stall) {
+        ctx->inject_stall = false;
+        *ctx->stall_flag = 0u;
+        hipLaunchKernelGGL(k_stalled_collective, dim3(1), dim3(64), 0, s, ctx->stall_flag_dev,
+                           (uint64_t)60 * 100000000ull);   // wall_clock64 runs at 100 MHz
+        FRI_HIP(ctx, hipGetLastError());
+        return FRI_OK;
+    }
     if (!tp.host) {
         FRI_NCCL(ctx, ncclGroupStart());
         for (int p = 0; p < tp.world; p++) {
@@ -1276,6 +1459,26 @@ extern "C" int fri_dist_detach(fri_ctx* ctx) {
     return FRI_OK;
 }
 
+extern "C" int fri_dist_info(fri_ctx* ctx, int* rank, int* world, int* transport) {
+    if (!ctx || !rank || !world || !transport) return fail(ctx, FRI_EINVAL, "null argument");
+    const Transport& tp = ctx->tp;
+    if (tp.host) {
+        *transport = FRI_TRANSPORT_HOST;
+        *rank = tp.rank;
+        *world = tp.world;
+    } else if (tp.comm) {
+        // what the communicator itself reports, not what attach was told
+        *transport = FRI_TRANSPORT_RCCL;
+        FRI_NCCL(ctx, ncclCommCount(tp.comm, world));
+        FRI_NCCL(ctx, ncclCommUserRank(tp.comm, rank));
+    } else {
+        *transport = FRI_TRANSPORT_NONE;
+        *rank = 0;
+        *world = 1;
+    }
+    return FRI_OK;
+}
+
 static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords);
 
 // Transport self-test: all-to-all, all-gather and a pair exchange on both
@@ -1291,14 +1494,18 @@ extern "C" int fri_dist_selftest(fri_ctx* ctx, size_t words_per_peer) {
     int rc = dist_buffers(ctx, tot, G, tot);
     if (rc) return rc;
     FRI_HIP(ctx, hipSetDevice(ctx->device));
-    std::vector<uint32_t> h(tot), got(tot);
+    // read-backs land in pinned staging: a copy into pageable memory would
+    // block the host behind a stalled collective before sync_sharded's deadline
+    if ((rc = tp_host_stage(ctx, tot * 4))) return rc;
+    std::vector<uint32_t> h(tot);
     for (uint32_t p = 0; p < G; p++)
         for (size_t i = 0; i < W; i++) h[p * W + i] = (r << 24) | (p << 16) | (uint32_t)i;
     hipStream_t s = ctx->stream;
     DistBuf& db = ctx->db;
     auto check = [&](const char* what, auto expect) -> int {
-        FRI_HIP(ctx, hipMemcpyAsync(got.data(), db.recv, tot * 4, hipMemcpyDeviceToHost, s));
+        FRI_HIP(ctx, hipMemcpyAsync(ctx->tp.hs, db.recv, tot * 4, hipMemcpyDeviceToHost, s));
         if (int rs = sync_sharded(ctx, s)) return rs;
+        const uint32_t* got = reinterpret_cast<const uint32_t*>(ctx->tp.hs);
         for (uint32_t p = 0; p < G; p++)
             for (size_t i = 0; i < W; i++)
                 if (got[p * W + i] != expect(p, (uint32_t)i))
@@ -1326,24 +1533,24 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
     DistBuf& b = ctx->db;
     const size_t nhi = 1u << 20;   // pow table hi part, generous (M <= 2^32)
     if (b.cap < M) {
-        hipFree(b.cyc); hipFree(b.recv); hipFree(b.half);
+        dfree(ctx, b.cyc); dfree(ctx, b.recv); dfree(ctx, b.half);
         b.cyc = b.recv = b.half = nullptr;
         b.cap = 0;
-        FRI_HIP(ctx, hipMalloc(&b.cyc, M * 4));
-        FRI_HIP(ctx, hipMalloc(&b.recv, M * 4));
-        FRI_HIP(ctx, hipMalloc(&b.half, (M / 2 + 1) * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.cyc, M * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.recv, M * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.half, (M / 2 + 1) * 4));
         b.cap = M;
     }
     if (!b.roots) {
-        FRI_HIP(ctx, hipMalloc(&b.roots, 64 * 32));
-        FRI_HIP(ctx, hipMalloc(&b.top, (size_t)(MAXR + 1) * 2 * 64 * 32));
-        FRI_HIP(ctx, hipMalloc(&b.pre_lo, ((size_t)1 << POW_LO_LOG) * 4));
-        FRI_HIP(ctx, hipMalloc(&b.pre_hi, nhi * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.roots, 64 * 32));
+        FRI_HIP(ctx, dalloc(ctx, &b.top, (size_t)(MAXR + 1) * 2 * 64 * 32));
+        FRI_HIP(ctx, dalloc(ctx, &b.pre_lo, ((size_t)1 << POW_LO_LOG) * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.pre_hi, nhi * 4));
     }
     if (b.gcap < gwords) {
-        hipFree(b.gath);
+        dfree(ctx, b.gath);
         b.gath = nullptr;
-        FRI_HIP(ctx, hipMalloc(&b.gath, gwords * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.gath, gwords * 4));
         b.gcap = gwords;
     }
     if (!ctx->xstream) {
@@ -1360,8 +1567,6 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
     return FRI_OK;
 }
 
-constexpr uint32_t SHARD_MIN_LOG = 20;   // layers of >= 2^20 elements are hashed sharded
-
 static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
                               uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                               const uint32_t* forced_betas, fri_commit_result* out) {
@@ -1373,7 +1578,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     if (G == 1 || log_n < SHARD_MIN_LOG || log_n < logG + 12)
         return run_commit(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
     if (!ctx->tp.host && !ctx->tp.comm) return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
-    if (log_n > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n out of range for context");
+    // a rank holds 1/G of the codeword: its NTT, twiddles and scratch are block-sized
+    if (log_n - logG > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n - log2(world) out of range for context");
     const size_t n = (size_t)1 << log_n;
     if (d > n) return fail(ctx, FRI_EDEGREE, "more coefficients than domain points (domain would be exhausted)");
     if (offset == 0 || offset >= P) return fail(ctx, FRI_EINVAL, "offset must be a nonzero canonical element");
@@ -1382,12 +1588,12 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     if (forced_betas && (flags & FRI_FLAG_FORCE_BETAS) && !check_canonical(forced_betas, MAXR))
         return fail(ctx, FRI_EINVAL, "forced beta not canonical");
     FRI_HIP(ctx, hipSetDevice(ctx->device));
-    int rc = plan_build(ctx, d, log_n, offset);
+    int rc = plan_build(ctx, d, log_n, offset, G, rank);
     if (rc) return rc;
     Plan& p = ctx->plan;
     hipStream_t s = ctx->stream;
     const size_t M = n / G;                                   // coset / block size of layer 0
-    rc = dist_buffers(ctx, M, G, (size_t)1 << SHARD_MIN_LOG);
+    rc = dist_buffers(ctx, M, G, (size_t)1 << (log_n - (uint32_t)p.k_sw));   // the layer gathered at the switch
     if (rc) return rc;
     DistBuf& db = ctx->db;
     ctx->sharded_layers = (uint32_t)p.rmax + 1;      // lowered when the tail goes local
@@ -1445,7 +1651,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         const size_t B = (size_t)1 << (Lk - logG);       // block size
         uint32_t* vals = p.layers + p.layer_off[k];     // my block at the start of the layer slot
         const bool last = (k == p.rmax);
-        const bool next_sharded = !last && (Lk - 1) >= SHARD_MIN_LOG && (Lk - 1 - logG) >= 10;
+        const bool next_sharded = next_layer_sharded(log_n, logG, k, p.rmax);
         // exchange of the half-block the partner needs for the next fold (overlaps the local tree)
         const uint32_t b = block_of[rank];
         const bool isA = b < G / 2;
@@ -1510,16 +1716,14 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         if (last) break;
         if (next_sharded) {
             if (!ctx->tp.host) FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_xchg, 0));
-            const size_t bb = isA ? b : b - G / 2;
             const uint32_t* first = isA ? vals : db.half;
             const uint32_t* second = isA ? db.half : vals + B / 2;
-            const uint32_t* xi = p.xinv + p.xinv_off[k] + bb * B + (isA ? 0 : B / 2);
+            // the plan's slot k holds exactly this rank's x^-1 half-block slice
+            if (fold_xinv_start(b, G, B) != p.xinv_start[k])
+                return fail(ctx, FRI_ESTATE, "shard plan out of step with the block schedule");
+            const uint32_t* xi = p.xinv + p.xinv_off[k];
             launch_pair_fold(first, second, xi, p.layers + p.layer_off[k + 1], B / 2, ctx->d_state, k, s);
-            for (uint32_t r = 0; r < G; r++) {
-                const uint32_t br = block_of[r];
-                block_of[r] = br < G / 2 ? 2 * br : 2 * (br - G / 2) + 1;
-            }
-            for (uint32_t r = 0; r < G; r++) rank_of[block_of[r]] = r;
+            advance_blocks(block_of, rank_of, G);
             continue;
         }
         // switch to local: gather layer k in block order, then the 1-GPU pipeline from k+1

@@ -113,11 +113,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_get_profile": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "fri_reset_profile": (i32, [vp]),
+        "fri_debug_inject_stall": (i32, [vp, i32]),
+        "fri_ctx_device_bytes": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "fri_debug_stamps": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), sz]),
         "fri_dist_unique_id": (i32, [ctypes.c_char_p]),
         "fri_dist_attach_rccl": (i32, [vp, i32, i32, ctypes.c_char_p]),
         "fri_dist_attach_host": (i32, [vp, i32, i32, ctypes.POINTER(Collectives)]),
         "fri_dist_detach": (i32, [vp]),
+        "fri_dist_info": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "fri_dist_selftest": (i32, [vp, sz]),
         "fri_commit_sharded": (i32, [vp, pu32, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
                                      ctypes.POINTER(CommitResult)]),
@@ -416,6 +419,13 @@ class Context:
     def detach(self):
         self._check(self.lib.fri_dist_detach(self.h))
 
+    def dist_info(self):
+        """(rank, world, transport) as the attached transport reports them
+        (transport: "none", "rccl" or "host"; fri_dist_info)."""
+        r, w, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._check(self.lib.fri_dist_info(self.h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(t)))
+        return r.value, w.value, ("none", "rccl", "host")[t.value]
+
     def dist_selftest(self, words_per_peer: int = 4096):
         self._check(self.lib.fri_dist_selftest(self.h, words_per_peer))
 
@@ -447,6 +457,12 @@ class Context:
 
     def reset_profile(self):
         self._check(self.lib.fri_reset_profile(self.h))
+
+    def device_bytes(self):
+        """(current, peak) HBM bytes held by this context (fri_ctx_device_bytes)."""
+        cur, peak = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.fri_ctx_device_bytes(self.h, ctypes.byref(cur), ctypes.byref(peak)))
+        return cur.value, peak.value
 
 
 # ----------------------------------------------------------------------------

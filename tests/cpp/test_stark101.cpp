@@ -7,6 +7,7 @@
 //   gpu: fri_commit / decommit_fri / MerkleTree / interpolate / batch
 //        inverse through libfri_amd.so against tests/golden (bit-exact).
 // Usage: test_stark101 [cpu|gpu|all]; exit status = number of failures.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -361,6 +362,53 @@ TEST(gpu, fri_commit_and_decommit_match_golden) {
         checked++;
     }
     ASSERT_TRUE(checked >= 30);
+}
+// The FRIProof's device-resident MerkleTree (get_authentication_path ->
+// fri_auth_path, one gather launch) and the query gather (fri_decommit_query)
+// serve the same rs_merkle paths, and each path hashes up to its layer root.
+TEST(gpu, auth_path_entry_points_agree) {
+    const uint32_t log_n = 16;
+    std::vector<FE> cs;
+    uint64_t x = 99;
+    for (size_t i = 0; i < (size_t{1} << (log_n - 3)); i++) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        cs.push_back(FE(x >> 33));
+    }
+    auto gpu = Gpu::thread_default(log_n);
+    FriChannel ch;
+    FRIProof proof = fri_commit_coset(Poly(cs), log_n, FE(5), ch, gpu);
+    const size_t nl = proof.n_layers();
+    std::vector<uint32_t> vals(2 * nl);
+    std::vector<uint8_t> paths(64 * 32 * nl);
+    for (uint64_t index : {uint64_t{0}, uint64_t{1}, uint64_t{12345}, (uint64_t{1} << log_n) - 1}) {
+        size_t plen = 0;
+        gpu->check(fri_decommit_query(gpu->ctx(), index, vals.data(), vals.size(), paths.data(), paths.size(), &plen),
+                   "fri_decommit_query");
+        size_t off = 0;
+        for (size_t k = 0; k < nl; k++) {
+            const uint32_t L = log_n - static_cast<uint32_t>(k);
+            const uint64_t idx = index % (uint64_t{1} << L);
+            auto ap = proof.fri_merkles[k].get_authentication_path(idx);
+            ASSERT_EQ(ap.size(), size_t{32} * L);
+            ASSERT_TRUE(std::equal(ap.begin(), ap.end(), paths.begin() + off));
+            // leaf -> root with the tree's own digest order (merkle/mod.rs:14-19)
+            uint8_t be[8] = {0, 0, 0, 0, uint8_t(vals[2 * k] >> 24), uint8_t(vals[2 * k] >> 16),
+                             uint8_t(vals[2 * k] >> 8), uint8_t(vals[2 * k])};
+            auto h = sha::digest(be, 8);
+            uint64_t j = idx;
+            for (uint32_t l = 0; l < L; l++) {
+                uint8_t buf[64];
+                const uint8_t* sib = ap.data() + 32 * l;
+                std::memcpy(buf + ((j & 1) ? 32 : 0), h.data(), 32);
+                std::memcpy(buf + ((j & 1) ? 0 : 32), sib, 32);
+                h = sha::digest(buf, 64);
+                j >>= 1;
+            }
+            ASSERT_EQ(sha::hex(h.data(), 32), proof.fri_merkles[k].root());
+            off += size_t{64} * L;
+        }
+        ASSERT_EQ(off, plen);
+    }
 }
 TEST(gpu, layers_lde_interpolate_merkle) {
     const GoldenCase* c = nullptr;

@@ -7,6 +7,9 @@ MODE "model": CPU model of the sharded commit (tests/dist_model.py) with the
               C oracle doing the per-block work and gloo doing the exchanges.
 MODE "gpu":   libfri_amd.so fri_commit_sharded on GPU 0 (every rank shares
               the one GPU), collectives staged through the host over gloo.
+MODE "gpu_shard": the same on a context sized for one rank's shard only
+              (log_n_max = log_n - log2 W; BASELINE configs[4] is 2^28 over
+              8 ranks); reports the rank's HBM bytes, no 1-GPU re-commit.
 Each rank writes OUT_DIR/rank<r>.json with its transcript-visible result.
 """
 import json
@@ -30,8 +33,34 @@ def main():
 
     import fri_oracle as fo
     d = (1 << log_n) >> blowup_log
-    coeffs = fo.splitmix64_field(seed, d)
-    if mode == "model":
+    coeffs = fo.splitmix64_np(seed, d) if mode == "gpu_shard" else fo.splitmix64_field(seed, d)
+    if mode == "gpu_shard":
+        import time
+        import fri_amd
+        logw = world.bit_length() - 1
+        t0 = time.monotonic()
+        ctx = fri_amd.Context(0, log_n - logw)
+        ctx.attach_torch(rank, world)
+        ctx.dist_selftest(1024)
+        r = ctx.commit_sharded(coeffs, log_n)
+        cur, peak = ctx.device_bytes()
+        res = {"roots": [bytes(r.roots[k]).hex() for k in range(r.n_layers)],
+               "betas": [int(r.betas[i]) for i in range(r.n_rounds)],
+               "final_value": int(r.final_value), "final_degree": int(r.final_degree),
+               "state": bytes(r.channel_out.digest).hex(), "hbm_bytes": cur, "hbm_peak_bytes": peak,
+               "ctx_log_n_max": log_n - logw, "seconds": round(time.monotonic() - t0, 2)}
+        try:
+            ctx.layer(0, log_n)
+            res["layer0_refused"] = False
+        except fri_amd.FriError:
+            res["layer0_refused"] = True
+        last = r.n_layers - 1
+        res["last_layer_constant"] = bool((ctx.layer(last, log_n) == r.final_value).all())
+        print(f"[rank {rank}] 2^{log_n} sharded over {world}: {res['seconds']} s, HBM {peak / 2**30:.2f} GiB",
+              file=sys.stderr, flush=True)
+        ctx.detach()
+        ctx.close()
+    elif mode == "model":
         import dist_model
         res = dist_model.sharded_commit(coeffs, log_n, rank, world, shard_min_log=int(os.environ.get("SHARD_MIN", "8")))
     else:

@@ -24,7 +24,7 @@ def free_port():
     return p
 
 
-def run_ranks(mode, world, log_n, seed, timeout, env_extra=None, blowup_log=3):
+def run_ranks(mode, world, log_n, seed, timeout, env_extra=None, blowup_log=3, stream_stderr=False):
     out = tempfile.mkdtemp(prefix=f"fri_{mode}_")
     env = dict(os.environ)
     env["MASTER_ADDR"] = "127.0.0.1"
@@ -32,8 +32,9 @@ def run_ranks(mode, world, log_n, seed, timeout, env_extra=None, blowup_log=3):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "dist_worker.py"), mode, str(log_n), str(seed), out, str(blowup_log)]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
-    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None if stream_stderr else subprocess.PIPE,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, (r.stderr or "")[-3000:]
     res = [json.load(open(os.path.join(out, f"rank{i}.json"))) for i in range(world)]
     return res
 
@@ -100,24 +101,122 @@ def test_rccl_transport_selftest_world1():
         ctx.close()
 
 
+def _run_child(code, timeout=180):
+    """Run `code` in a fresh interpreter (its own HIP context and RCCL state:
+    a rendezvous thread abandoned there cannot leak into other tests) and
+    return the JSON object it prints last."""
+    env = dict(os.environ)
+    env["FRI_RCCL_TIMEOUT_S"] = "3"
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "stark-prover_amd", "python"),
+                                         os.path.join(ROOT, "oracle"), env.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+_ATTACH_TIMEOUT_CHILD = r"""
+import json, os, time
+import fri_amd, fri_oracle as fo
+ctx = fri_amd.Context(0, 20)
+t0 = time.monotonic()
+try:
+    ctx.attach_rccl(0, 2, fri_amd.Context.unique_id())
+    out = {"raised": False}
+except fri_amd.FriError as e:
+    out = {"raised": True, "code": e.code, "msg": str(e)}
+out["seconds"] = time.monotonic() - t0
+out["n_layers"] = int(ctx.commit(fo.splitmix64_field(3, 128), 10).n_layers)
+print(json.dumps(out), flush=True)
+os._exit(0)   # the abandoned setup thread is still blocked in RCCL's bootstrap
+"""
+
+
 @pytest.mark.gpu
-def test_rccl_attach_times_out_without_peer(monkeypatch, oracle):
+def test_rccl_attach_times_out_without_peer():
     """A rendezvous that never completes (rank 0 of 2, rank 1 absent) ends in
     FRI_ERCCL after FRI_RCCL_TIMEOUT_S instead of hanging, and the context
-    stays usable for 1-GPU commits.  (The abandoned setup thread stays blocked
-    in RCCL's bootstrap for the rest of the process: keep this test last among
-    the RCCL tests.)"""
-    import time
+    stays usable for 1-GPU commits.  Runs in a child process: the abandoned
+    setup thread stays blocked in RCCL's bootstrap until that process exits."""
     import fri_amd
-    monkeypatch.setenv("FRI_RCCL_TIMEOUT_S", "3")
-    ctx = fri_amd.Context(0, 20)
-    try:
-        t0 = time.monotonic()
-        with pytest.raises(fri_amd.FriError, match="rendezvous"):
-            ctx.attach_rccl(0, 2, fri_amd.Context.unique_id())
-        assert time.monotonic() - t0 < 60
-        coeffs = oracle.splitmix64_field(3, 128)
-        res = ctx.commit(coeffs, 10)
-        assert res.n_layers == 8
-    finally:
-        ctx.close()
+    r = _run_child(_ATTACH_TIMEOUT_CHILD)
+    assert r["raised"] and r["code"] == fri_amd.FRI_ERCCL and "rendezvous" in r["msg"]
+    assert r["seconds"] < 60
+    assert r["n_layers"] == 8
+
+
+_STALL_CHILD = r"""
+import json, os, time
+import fri_amd, fri_oracle as fo
+ctx = fri_amd.Context(0, 16)
+ctx.attach_rccl(0, 1, fri_amd.Context.unique_id())
+ctx.dist_selftest(1024)                                   # the transport works
+ctx._check(ctx.lib.fri_debug_inject_stall(ctx.h, 1))      # next all-to-all never completes
+out = {}
+t0 = time.monotonic()
+try:
+    ctx.dist_selftest(1024)
+    out["first"] = None
+except fri_amd.FriError as e:
+    out["first"] = [e.code, str(e)]
+out["seconds"] = time.monotonic() - t0
+try:
+    ctx.dist_selftest(1024)
+    out["second"] = None
+except fri_amd.FriError as e:
+    out["second"] = [e.code, str(e)]
+c = fo.splitmix64_field(3, 1 << 11)
+out["commit_layers"] = int(ctx.commit(c, 14).n_layers)     # the context still commits on one GPU
+ctx.close()
+print(json.dumps(out), flush=True)
+"""
+
+
+@pytest.mark.gpu
+def test_rccl_collective_stall_aborts():
+    """A collective that never completes (injected: the all-to-all replaced
+    by a kernel that waits like one whose peer is gone) ends in FRI_ERCCL
+    within FRI_RCCL_TIMEOUT_S: the deadline polls the stream, aborts the
+    communicators (which releases the waiting kernel) and drains the stream;
+    the next sharded call finds no transport (FRI_ESTATE); 1-GPU commits on
+    the same context still work."""
+    import fri_amd
+    r = _run_child(_STALL_CHILD)
+    assert r["first"] is not None and r["first"][0] == fri_amd.FRI_ERCCL, r
+    assert "no progress" in r["first"][1] and "still busy" not in r["first"][1]
+    assert 2.5 < r["seconds"] < 30
+    assert r["second"] is not None and r["second"][0] == fri_amd.FRI_ESTATE
+    assert r["commit_layers"] == 12
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(1200)
+def test_sharded_2p28_world8_configs4(oracle_commit):
+    """BASELINE configs[4]: a 2^28 codeword (d = 2^25) committed coset-sharded
+    by 8 ranks (host transport over gloo, all 8 sharing GPU 0), each rank on a
+    shard-sized context (log_n_max 25): every root, beta, the final value and
+    the channel state equal the OpenMP C oracle's 1-node commit, on every rank,
+    and each rank holds well under 1/8 of the ~38 GB a 1-GPU 2^28 commit needs."""
+    got = run_ranks("gpu_shard", 8, 28, 8, timeout=1100, stream_stderr=True)
+    want = oracle_commit(28, 8)
+    for r in got:
+        assert r["roots"] == want["roots"]
+        assert r["betas"] == want["betas"]
+        assert r["final_value"] == want["final_value"] and r["final_degree"] == want["final_degree"]
+        assert r["state"] == want["state"]
+        assert r["layer0_refused"] and r["last_layer_constant"]
+        assert r["hbm_peak_bytes"] < 8 * 2**30, r["hbm_peak_bytes"]
+    print("per-rank HBM (GiB):", [round(r["hbm_peak_bytes"] / 2**30, 2) for r in got])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,log_n", [(2, 22), (4, 23), (8, 24)])
+def test_sharded_shard_sized_context(world, log_n, oracle_commit):
+    """Shard-sized contexts (log_n_max = log_n - log2 world) at smaller sizes:
+    the same transcript as the oracle, and per-rank HBM well below what the
+    whole-codeword plan needed (layers + trees alone are ~130 * 2^log_n bytes)."""
+    got = run_ranks("gpu_shard", world, log_n, 11, timeout=900)
+    want = oracle_commit(log_n, 11)
+    for r in got:
+        assert {k: r[k] for k in want} == want
+        assert r["layer0_refused"] and r["last_layer_constant"]
+        assert r["hbm_peak_bytes"] < 130 * (1 << log_n) / world + (512 << 20), r["hbm_peak_bytes"]
