@@ -52,6 +52,8 @@ struct Plan {
     int32_t* wgmax = nullptr;       // per-workgroup coefficient maxima
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    hipGraph_t tail_graph = nullptr;        // sharded plan: the local layers after the switch
+    hipGraphExec_t tail_exec = nullptr;
     bool graph_profiled = false;
 };
 
@@ -259,6 +261,8 @@ static void plan_free(fri_ctx* ctx) {
     Plan& p = ctx->plan;
     if (p.exec) hipGraphExecDestroy(p.exec);
     if (p.graph) hipGraphDestroy(p.graph);
+    if (p.tail_exec) hipGraphExecDestroy(p.tail_exec);
+    if (p.tail_graph) hipGraphDestroy(p.tail_graph);
     dfree(ctx, p.d_in); dfree(ctx, p.coefA); dfree(ctx, p.coefB); dfree(ctx, p.layers);
     dfree(ctx, p.trees); dfree(ctx, p.xinv); dfree(ctx, p.pre_lo); dfree(ctx, p.pre_hi); dfree(ctx, p.wgmax);
     p = Plan();
@@ -1256,10 +1260,12 @@ __global__ void k_stalled_collective(const uint32_t* flag, uint64_t max_ticks) {
 
 static void rccl_abort(fri_ctx* ctx) {
     Transport& tp = ctx->tp;
+    // an injected stall is released first, as ncclCommAbort's abort flag
+    // releases a real RCCL kernel before the abort waits for the device
+    if (ctx->stall_flag) __atomic_store_n(ctx->stall_flag, 1u, __ATOMIC_SEQ_CST);
     if (tp.xcomm) ncclCommAbort(tp.xcomm);
     if (tp.comm) ncclCommAbort(tp.comm);
     tp.comm = tp.xcomm = nullptr;      // the transport is gone: later sharded calls see FRI_ESTATE
-    if (ctx->stall_flag) __atomic_store_n(ctx->stall_flag, 1u, __ATOMIC_SEQ_CST);   // ends an injected stall
 }
 #define FRI_NCCL(ctx, expr)                                                                  \
     do {                                                                                     \
@@ -1731,18 +1737,40 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         sp = span_begin(ctx, "gather", B * 4 * G);
         rc = tp_allgather(ctx, vals, db.gath, B * 4, s);
         if (rc) return rc;
-        for (uint32_t r = 0; r < G; r++)
-            FRI_HIP(ctx, hipMemcpyAsync(p.layers + p.layer_off[k] + (size_t)block_of[r] * B, db.gath + (size_t)r * B,
-                                        B * 4, hipMemcpyDeviceToDevice, s));
-        for (int kk = k + 1; kk <= p.rmax; kk++) {
-            if (log_n - (uint32_t)kk <= TAIL_LOG) {      // small layers: one launch
-                LayerTask ts[TAIL_LOG + 1];
-                uint32_t nt = 0;
-                for (int k2 = kk; k2 <= p.rmax; k2++) ts[nt++] = commit_task(ctx, k2);
-                launch_tail(ts, nt, s);
-                break;
+        // the gathered blocks into place and the local layers: the same
+        // launches on every commit of this plan (block_of at the switch is
+        // fixed by (G, rank)), so they replay as one hipGraph captured on the
+        // first commit, without a launch gap per kernel
+        auto local_tail = [&]() -> int {
+            for (uint32_t r = 0; r < G; r++)
+                FRI_HIP(ctx, hipMemcpyAsync(p.layers + p.layer_off[k] + (size_t)block_of[r] * B,
+                                            db.gath + (size_t)r * B, B * 4, hipMemcpyDeviceToDevice, s));
+            for (int kk = k + 1; kk <= p.rmax; kk++) {
+                if (log_n - (uint32_t)kk <= TAIL_LOG) {      // small layers: one launch
+                    LayerTask ts[TAIL_LOG + 1];
+                    uint32_t nt = 0;
+                    for (int k2 = kk; k2 <= p.rmax; k2++) ts[nt++] = commit_task(ctx, k2);
+                    launch_tail(ts, nt, s);
+                    break;
+                }
+                launch_layer(commit_task(ctx, kk), s);
             }
-            launch_layer(commit_task(ctx, kk), s);
+            return FRI_OK;
+        };
+        if (ctx->profiling || (flags & FRI_FLAG_NO_GRAPH)) {
+            if ((rc = local_tail())) return rc;
+        } else {
+            if (!p.tail_exec) {
+                FRI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+                rc = local_tail();
+                hipGraph_t g = nullptr;
+                const hipError_t ec = hipStreamEndCapture(s, &g);
+                if (rc) return rc;
+                FRI_HIP(ctx, ec);
+                p.tail_graph = g;
+                FRI_HIP(ctx, hipGraphInstantiate(&p.tail_exec, g, nullptr, nullptr, 0));
+            }
+            FRI_HIP(ctx, hipGraphLaunch(p.tail_exec, s));
         }
         span_end(ctx, sp);
         break;

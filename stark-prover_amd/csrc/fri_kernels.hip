@@ -53,6 +53,9 @@ __device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4) 
 #ifndef NTT_TPB
 #define NTT_TPB 512          // threads per NTT tile (16 elements each; 512: 128-byte row runs)
 #endif
+#ifndef NTT_WIDE
+#define NTT_WIDE 1           // first pass of 9..12 stages instead of a 1..4-stage pass (k_ntt_first_wide)
+#endif
 
 // Z (FIRST only): the input has d <= n / 2^Z coefficients, so after the
 // bit-reversal gather every row q with q mod 2^Z != 0 is zero and DIT stages
@@ -263,6 +266,183 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
     }
 }
 
+// First pass with NS = 9..12 stages (k_ntt_first_wide).  A transform of
+// 2^log_n with log_n mod 8 in 1..4 would otherwise start with a 1..4-stage
+// pass that reads and writes the whole codeword for a few stages (2^25: 1 of
+// 4 passes, 2^28: 4): this pass takes those stages together with the next 8.
+// Same tile as k_ntt_pass (512 threads x 16 elements), now P = 2^NS rows x
+// C = 8192 / P columns, in three register phases of 4, 4 and NS - 8 stages
+// with two LDS exchanges between them.  The loads are the bit-reversed input
+// rows (C consecutive words each, only the rows that are nonzero for d <=
+// n / 2^Z), the stores whole contiguous columns of P words (16-byte vectors).
+template <int NS, int TPB, int Z>
+__global__ __launch_bounds__(TPB) void k_ntt_first_wide(const uint32_t* src, size_t d, uint32_t* dst, uint32_t log_n,
+                                                        const uint32_t* __restrict__ tw,
+                                                        const uint32_t* __restrict__ pre_lo,
+                                                        const uint32_t* __restrict__ pre_hi,
+                                                        const uint32_t* __restrict__ post_lo,
+                                                        const uint32_t* __restrict__ post_hi) {
+    static_assert(NS >= 9 && NS <= 12 && Z <= 3, "wide first pass: 9..12 stages");
+    constexpr uint32_t P = 1u << NS, TILE = 16u * TPB, C = TILE / P;
+    constexpr uint32_t VW = C < 4 ? C : 4;         // words per input vector (C consecutive words per row)
+    constexpr uint32_t VPR = C / VW;               // input vectors per row
+    constexpr uint32_t B2 = NS - 8;                // stages of phase 2
+    __shared__ uint32_t lds[TILE + TILE / 16 + 2 * (TILE >> 10)];
+    __shared__ uint32_t tws[P];                    // tw[0 .. 2^NS): w_{2^(t+1)}^j at 2^t + j
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < P; i += TPB) tws[i] = tw[i];
+    const size_t col0 = (size_t)blockIdx.x * C;
+    const uint32_t cbits = log_n - NS;
+    // ---- load: rows q = q' 2^Z (the others are zero), VW words per lane ----
+    constexpr uint32_t NV = (P >> Z) * VPR;
+    for (uint32_t v = tid; v < NV; v += TPB) {
+        const uint32_t c = (v % VPR) * VW, q = (v / VPR) << Z;
+        const size_t si = ((size_t)(__brev(q) >> (32 - NS)) << cbits) + col0 + c;
+        uint32_t w[VW];
+#pragma unroll
+        for (uint32_t i = 0; i < VW; i++) w[i] = 0u;
+        if (si + VW <= d) {
+            if (VW == 4) {
+                const uint4 x = *reinterpret_cast<const uint4*>(src + si);
+                w[0] = x.x; w[1 % VW] = x.y; w[2 % VW] = x.z; w[3 % VW] = x.w;
+            } else if (VW == 2) {
+                const uint2 x = *reinterpret_cast<const uint2*>(src + si);
+                w[0] = x.x; w[1 % VW] = x.y;
+            } else {
+                w[0] = src[si];
+            }
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < VW; i++) w[i] = si + i < d ? src[si + i] : 0u;
+        }
+        if (pre_lo) {
+#pragma unroll
+            for (uint32_t i = 0; i < VW; i++)
+                if (si + i < d) w[i] = pow2lvl(pre_lo, pre_hi, si + i, w[i]);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < VW; i++) lds[ntt_laddr((c + i) * P + q)] = w[i];
+    }
+    __syncthreads();
+    uint32_t r[16];
+    auto twid = [&](int t, uint32_t q0) -> uint32_t { return tws[(1u << t) + (q0 & ((1u << t) - 1))]; };
+    // ---- phase 0: stages 0..3 on 16 consecutive rows (0..Z-1 are copies) ----
+#pragma unroll
+    for (int e = 0; e < 16; e++) r[e] = (e & ((1 << Z) - 1)) ? 0u : lds[ntt_laddr(tid * 16 + e)];
+#pragma unroll
+    for (int e = 0; e < 16; e++) r[e] = r[e & ~((1 << Z) - 1)];
+    {
+        const uint32_t x0 = tid * 16;
+#pragma unroll
+        for (int t = Z; t < 4; t++) {
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+                if (e & (1 << t)) continue;
+                const uint32_t u = r[e];
+                // x0 is a multiple of 16: the twiddle of e mod 2^t == 0 is 1
+                const uint32_t v = (e & ((1 << t) - 1)) == 0 ? r[e + (1 << t)]
+                                                              : mmul(r[e + (1 << t)], twid(t, (x0 + e) & (P - 1)));
+                r[e] = add(u, v);
+                r[e + (1 << t)] = sub(u, v);
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 16; e++) lds[ntt_laddr(tid * 16 + e)] = r[e];
+    __syncthreads();
+    // ---- phase 1: stages 4..7, one group of 16 rows at stride 16 per thread --
+    {
+        const uint32_t ql = tid & 15, qh = (tid >> 4) & ((1u << (NS - 8)) - 1), c = tid >> (NS - 4);
+        const uint32_t base = c * P + ql + qh * 256;
+#pragma unroll
+        for (int m = 0; m < 16; m++) r[m] = lds[ntt_laddr(base + m * 16)];
+#pragma unroll
+        for (int t = 4; t < 8; t++) {
+            const int tb = t - 4;
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                if (m & (1 << tb)) continue;
+                const uint32_t u = r[m], v = mmul(r[m + (1 << tb)], twid(t, ql + ((uint32_t)m << 4)));
+                r[m] = add(u, v);
+                r[m + (1 << tb)] = sub(u, v);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++) lds[ntt_laddr(base + m * 16)] = r[m];
+    }
+    __syncthreads();
+    // ---- phase 2: stages 8..NS-1, groups of 2^B2 rows at stride 256; group
+    // g * TPB + tid, so the lanes of a wave read consecutive rows ----------
+    {
+        constexpr uint32_t GPT = 16u >> B2;
+#pragma unroll
+        for (uint32_t g = 0; g < GPT; g++) {
+            const uint32_t G = g * TPB + tid, c = G >> 8, ql = G & 255;
+#pragma unroll
+            for (uint32_t m = 0; m < (1u << B2); m++) r[g * (1u << B2) + m] = lds[ntt_laddr(c * P + ql + m * 256)];
+        }
+#pragma unroll
+        for (int t = 8; t < NS; t++) {
+            const int tb = t - 8;
+#pragma unroll
+            for (uint32_t g = 0; g < GPT; g++) {
+                const uint32_t ql = (g * TPB + tid) & 255;
+#pragma unroll
+                for (int m = 0; m < (1 << B2); m++) {
+                    if (m & (1 << tb)) continue;
+                    const int e = (int)g * (1 << B2) + m;
+                    const uint32_t u = r[e], v = mmul(r[e + (1 << tb)], twid(t, ql + ((uint32_t)m << 8)));
+                    r[e] = add(u, v);
+                    r[e + (1 << tb)] = sub(u, v);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t g = 0; g < GPT; g++) {
+            const uint32_t G = g * TPB + tid, c = G >> 8, ql = G & 255;
+#pragma unroll
+            for (uint32_t m = 0; m < (1u << B2); m++) lds[ntt_laddr(c * P + ql + m * 256)] = r[g * (1u << B2) + m];
+        }
+    }
+    __syncthreads();
+    // ---- store: tile column c is output column bitrev(col0 + c), P contiguous words
+#pragma unroll
+    for (uint32_t rr = 0; rr < 4; rr++) {
+        const uint32_t y = rr * TPB + tid;
+        const uint32_t c = y / (P / 4), q = (y % (P / 4)) * 4;
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) w[j] = lds[ntt_laddr(c * P + q + j)];
+        const size_t col = col0 + c;
+        const size_t g = (size_t)(cbits ? (__brev((uint32_t)col) >> (32 - cbits)) : 0u) * P + q;
+        if (post_lo) {
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) w[j] = pow2lvl(post_lo, post_hi, g + j, w[j]);
+        }
+        *reinterpret_cast<uint4*>(dst + g) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+template <int NS>
+static void launch_first_wide(const uint32_t* src, size_t d, uint32_t* dst, uint32_t log_n, const NttPlan& p,
+                              bool last, uint32_t z, hipStream_t s) {
+    constexpr int TPB = 512;
+    const unsigned blocks = (unsigned)(((size_t)1 << log_n) / (16 * TPB));
+    const uint32_t* qlo = last ? p.post_lo : nullptr;
+    const uint32_t* qhi = last ? p.post_hi : nullptr;
+    switch (z) {
+#define WIDE_CASE(ZV)                                                                                        \
+    case ZV:                                                                                                 \
+        hipLaunchKernelGGL((k_ntt_first_wide<NS, TPB, ZV>), dim3(blocks), dim3(TPB), 0, s, src, d, dst, log_n, \
+                           p.tw, p.pre_lo, p.pre_hi, qlo, qhi);                                              \
+        break;
+        WIDE_CASE(0) WIDE_CASE(1) WIDE_CASE(2) default: WIDE_CASE(3)
+#undef WIDE_CASE
+    }
+}
+
 __global__ void k_ntt_one(const uint32_t* src, size_t d, uint32_t* dst, const uint32_t* pre_lo,
                           const uint32_t* pre_hi, const uint32_t* post_lo, const uint32_t* post_hi) {
     if (threadIdx.x) return;
@@ -325,6 +505,25 @@ void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, 
     }
     uint32_t first = log_n % 8;
     if (first == 0) first = 8;
+#if NTT_WIDE
+    // a short first pass (1..4 stages) merged with the next 8: one pass fewer
+    if (first <= 4 && log_n >= 13 && log_n - first >= 8 &&
+        ((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
+        first += 8;
+        uint32_t z = 0;
+        while (z < 3 && ((size_t)d << (z + 1)) <= ((size_t)1 << log_n)) z++;
+        const bool last = first == log_n;
+        switch (first) {
+            case 9: launch_first_wide<9>(src, d, dst, log_n, p, last, z, s); break;
+            case 10: launch_first_wide<10>(src, d, dst, log_n, p, last, z, s); break;
+            case 11: launch_first_wide<11>(src, d, dst, log_n, p, last, z, s); break;
+            default: launch_first_wide<12>(src, d, dst, log_n, p, last, z, s); break;
+        }
+        for (uint32_t s0 = first; s0 < log_n; s0 += 8)
+            launch_pass<false>(8, dst, 0, dst, log_n, s0, p, s0 + 8 == log_n, s);
+        return;
+    }
+#endif
     launch_first(first, src, d, dst, log_n, p, first == log_n, s);
     for (uint32_t s0 = first; s0 < log_n; s0 += 8)
         launch_pass<false>(8, dst, 0, dst, log_n, s0, p, s0 + 8 == log_n, s);

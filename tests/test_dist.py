@@ -101,12 +101,13 @@ def test_rccl_transport_selftest_world1():
         ctx.close()
 
 
-def _run_child(code, timeout=180):
+def _run_child(code, timeout=180, rccl_timeout=True):
     """Run `code` in a fresh interpreter (its own HIP context and RCCL state:
     a rendezvous thread abandoned there cannot leak into other tests) and
     return the JSON object it prints last."""
     env = dict(os.environ)
-    env["FRI_RCCL_TIMEOUT_S"] = "3"
+    if rccl_timeout:
+        env["FRI_RCCL_TIMEOUT_S"] = "3"
     env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "stark-prover_amd", "python"),
                                          os.path.join(ROOT, "oracle"), env.get("PYTHONPATH", "")])
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=timeout)
@@ -148,8 +149,9 @@ _STALL_CHILD = r"""
 import json, os, time
 import fri_amd, fri_oracle as fo
 ctx = fri_amd.Context(0, 16)
-ctx.attach_rccl(0, 1, fri_amd.Context.unique_id())
+ctx.attach_rccl(0, 1, fri_amd.Context.unique_id())       # default deadline: a first RCCL init can take seconds
 ctx.dist_selftest(1024)                                   # the transport works
+os.environ["FRI_RCCL_TIMEOUT_S"] = "3"                    # read by the library at every deadline
 ctx._check(ctx.lib.fri_debug_inject_stall(ctx.h, 1))      # next all-to-all never completes
 out = {}
 t0 = time.monotonic()
@@ -180,7 +182,7 @@ def test_rccl_collective_stall_aborts():
     the next sharded call finds no transport (FRI_ESTATE); 1-GPU commits on
     the same context still work."""
     import fri_amd
-    r = _run_child(_STALL_CHILD)
+    r = _run_child(_STALL_CHILD, rccl_timeout=False)
     assert r["first"] is not None and r["first"][0] == fri_amd.FRI_ERCCL, r
     assert "no progress" in r["first"][1] and "still busy" not in r["first"][1]
     assert 2.5 < r["seconds"] < 30

@@ -54,7 +54,11 @@ def test_batch_inverse_edges(ctx):
                                      # n = 2^13; a first pass of 8 stages whose last loaded vector
                                      # straddles d (d mod 4 = 1, 2, 3), blowup 1, n = one tile
                                      (16, 8189), (16, 8190), (16, 8191), (16, 1 << 16), (13, 8191),
-                                     (13, 1 << 13), (24, (1 << 21) - 3)])
+                                     (13, 1 << 13), (24, (1 << 21) - 3),
+                                     # first pass of 9..12 stages (k_ntt_first_wide) with 3, 2, 1 and 0
+                                     # trivial stages, vectors straddling d, blowup 1
+                                     (17, 1 << 14), (17, 16385), (18, 32767), (19, 1 << 16), (19, (1 << 19) - 1),
+                                     (20, 1 << 19), (20, 1 << 20), (21, 1 << 18), (23, 12345)])
 def test_lde_matches_oracle(ctx, corc, log_n, d):
     c = rng_field(log_n * 100 + d, d)
     got = ctx.lde(c, log_n, 5)
@@ -106,7 +110,7 @@ def test_evaluate_few_points_many_coefficients(ctx, corc, d, count):
 
 
 # ------------------------------------------------------ poly: interpolate --
-@pytest.mark.parametrize("log_n", [0, 1, 2, 5, 10, 13, 16])
+@pytest.mark.parametrize("log_n", [0, 1, 2, 5, 10, 13, 16, 17, 20])
 def test_interpolate_roundtrip(ctx, corc, log_n):
     n = 1 << log_n
     c = rng_field(log_n + 5, n)
@@ -223,6 +227,34 @@ def test_merkle_root_matches_oracle(ctx, corc, oracle, n):
     assert got == buf.raw[32 * (cnt - 1):]
     if n <= 4096:
         assert got.hex() == oracle.merkle_root_hex([int(x) for x in v])
+
+
+def test_large_merkle_root_releases_scratch(corc, oracle):
+    """fri_merkle_root builds its tree in the context's grown scratch; a tree
+    past 256 MiB is released after the call, so a large root does not pin HBM
+    for the context's life and a large commit on the same context still fits
+    (16 GiB pinned after a 2^28 root)."""
+    import fri_amd
+    big = fri_amd.Context(0, 24)
+    try:
+        base = big.device_bytes()[0]
+        v = rng_field(23, 1 << 23)                    # tree of 2^24 digests: 512 MiB
+        got = big.merkle_root(v)
+        vs, pv = c_u64(v)
+        cnt = corc.orc_merkle_nodes_count(1 << 23)
+        buf = ctypes.create_string_buffer(32 * cnt)
+        corc.orc_merkle_build(pv, 1 << 23, buf)
+        assert got == buf.raw[32 * (cnt - 1):]
+        cur, peak = big.device_bytes()
+        assert cur == base and peak >= base + (512 << 20)
+        small = rng_field(11, 1 << 12)                # small trees keep their scratch (no hipFree per call)
+        big.merkle_root(small)
+        assert big.device_bytes()[0] > base
+        c = oracle.splitmix64_np(42, 1 << 21).astype(np.uint32)
+        res = big.commit(c, 24)
+        assert res.n_layers == 22
+    finally:
+        big.close()
 
 
 def test_merkle_tree_class(oracle):
