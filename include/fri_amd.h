@@ -307,6 +307,14 @@ int fri_ctx_device_bytes(fri_ctx* ctx, uint64_t* current, uint64_t* peak);
  * last commit, (FRI_MAX_LAYERS x 24) u64 ticks of the 100 MHz clock.
  * Returns FRI_ESTATE in the product build. */
 int fri_debug_stamps(fri_ctx* ctx, uint64_t* out, size_t cap);
+/* Host-only diagnostic (no context, no device): the commit plan's layout for
+ * rank `rank` of `world` (world 1: the 1-GPU plan) of a codeword 2^log_n with
+ * d coefficients.  out[0] = rounds bound R, out[1] = last sharded layer k_sw
+ * (-1 for world 1), out[2] = bytes of layers + trees + x^-1 tables; then per
+ * layer k <= R five words: layer-slot words, tree-slot words, x^-1 entries of
+ * fold k, the domain index of the first of them, the block held of sharded
+ * layer k.  cap >= 4 + 5 * FRI_MAX_LAYERS. */
+int fri_debug_plan_layout(size_t d, uint32_t log_n, uint32_t world, uint32_t rank, uint64_t* out, size_t cap);
 /* Test hook for the collective deadline (fri_dist_attach_rccl): with enable
  * != 0 the next RCCL all-to-all on the context is replaced by a kernel that
  * waits like a collective whose peer never arrives, until the deadline's

@@ -47,6 +47,7 @@ struct Plan {
     uint32_t* trees = nullptr;  size_t tree_off[MAXR + 2] = {0};
     uint32_t* xinv = nullptr;   size_t xinv_off[MAXR + 2] = {0};
     size_t xinv_start[MAXR + 2] = {0};   // domain index of xinv slot k's first entry (sharded slices)
+    uint32_t block[MAXR + 2] = {0};      // block this rank holds of sharded layer k (k <= k_sw)
     uint32_t* pre_lo = nullptr;
     uint32_t* pre_hi = nullptr;
     int32_t* wgmax = nullptr;       // per-workgroup coefficient maxima
@@ -667,19 +668,15 @@ static size_t fold_xinv_start(uint32_t b, uint32_t G, size_t B) {
 // of rank `rank` (see Plan::sharded); its x^-1 slots hold only the slices the
 // rank's folds read, computed directly as (offset^(2^k) w_{n_k}^i)^-1 (the
 // same values the whole-domain squaring chain gives: D_k = D_0^(2^k)).
-static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, uint32_t G = 1, uint32_t rank = 0) {
-    Plan& p = ctx->plan;
+// The plan's layout (offsets and sizes, no allocation): also what
+// fri_debug_plan_layout reports, so the shard schedule is checkable on a host.
+static void plan_layout(Plan& p, size_t d, uint32_t log_n, uint32_t G, uint32_t rank, size_t& lay, size_t& tre,
+                        size_t& xin) {
     const bool sharded = G > 1;
-    if (p.valid && p.d == d && p.log_n == log_n && p.offset == offset && p.sharded == sharded && p.G == G &&
-        p.rank == rank)
-        return FRI_OK;
-    plan_free(ctx);
-    const size_t n = (size_t)1 << log_n;
     uint32_t logG = 0;
     while ((1u << logG) < G) logG++;
     p.log_n = log_n;
     p.d = d;
-    p.offset = offset;
     p.rmax = rounds_bound(d, log_n);
     p.sharded = sharded;
     p.G = G;
@@ -688,7 +685,7 @@ static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, u
     const bool local_tail = sharded && p.k_sw < p.rmax;
     std::vector<uint32_t> block_of(G), rank_of(G);
     for (uint32_t r = 0; r < G; r++) block_of[r] = rank_of[r] = r;
-    size_t lay = 0, tre = 0, xin = 0;
+    lay = tre = xin = 0;
     for (int k = 0; k <= p.rmax; k++) {
         const uint32_t L = log_n - (uint32_t)k;
         const bool blk = sharded && k <= p.k_sw;               // block-local tree
@@ -697,6 +694,7 @@ static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, u
         p.tree_off[k] = tre;
         p.xinv_off[k] = xin;
         p.xinv_start[k] = 0;
+        p.block[k] = blk ? block_of[rank] : 0u;
         lay += (blk && !(k == p.k_sw && local_tail)) ? ((size_t)1 << Lt) : ((size_t)1 << L);
         tre += 8 * (((size_t)2 << Lt) - 1);
         if (k < p.rmax) {
@@ -712,6 +710,20 @@ static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, u
     }
     p.layer_off[p.rmax + 1] = lay;
     p.tree_off[p.rmax + 1] = tre;
+    p.xinv_off[p.rmax + 1] = xin;
+}
+
+static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, uint32_t G = 1, uint32_t rank = 0) {
+    Plan& p = ctx->plan;
+    const bool sharded = G > 1;
+    if (p.valid && p.d == d && p.log_n == log_n && p.offset == offset && p.sharded == sharded && p.G == G &&
+        p.rank == rank)
+        return FRI_OK;
+    plan_free(ctx);
+    const size_t n = (size_t)1 << log_n;
+    size_t lay, tre, xin;
+    plan_layout(p, d, log_n, G, rank, lay, tre, xin);
+    p.offset = offset;
     p.in_cap = d ? d : 1;
     p.coef_cap = d / 2 + 1;
     const size_t nhi = log_n > POW_LO_LOG ? ((size_t)1 << (log_n - POW_LO_LOG)) : 1;
@@ -1210,6 +1222,31 @@ extern "C" int fri_debug_inject_stall(fri_ctx* ctx, int enable) {
         *ctx->stall_flag = 1u;
     }
     ctx->inject_stall = enable != 0;
+    return FRI_OK;
+}
+extern "C" int fri_debug_plan_layout(size_t d, uint32_t log_n, uint32_t world, uint32_t rank, uint64_t* out,
+                                     size_t cap) {
+    if (!out || log_n < 1 || log_n > 30 || world < 1 || world > 64 || (world & (world - 1)) || rank >= world)
+        return FRI_EINVAL;
+    uint32_t logG = 0;
+    while ((1u << logG) < world) logG++;
+    if (world > 1 && log_n < logG + 12) return FRI_EINVAL;
+    if (cap < 4 + 5 * (size_t)(MAXR + 1)) return FRI_EINVAL;
+    Plan p;
+    size_t lay, tre, xin;
+    plan_layout(p, d, log_n, world, rank, lay, tre, xin);
+    out[0] = (uint64_t)p.rmax;
+    out[1] = (uint64_t)(int64_t)p.k_sw;
+    out[2] = 4 * (uint64_t)(lay + tre + xin);                 // bytes of layers + trees + x^-1 tables
+    out[3] = 0;
+    for (int k = 0; k <= p.rmax; k++) {
+        uint64_t* o = out + 4 + 5 * (size_t)k;
+        o[0] = p.layer_off[k + 1] - p.layer_off[k];            // words in layer slot k
+        o[1] = p.tree_off[k + 1] - p.tree_off[k];              // words in tree slot k
+        o[2] = p.xinv_off[k + 1] - p.xinv_off[k];              // x^-1 entries of fold k
+        o[3] = p.xinv_start[k];                                // domain index of the first
+        o[4] = p.block[k];                                     // block held of sharded layer k
+    }
     return FRI_OK;
 }
 extern "C" int fri_ctx_device_bytes(fri_ctx* ctx, uint64_t* current, uint64_t* peak) {

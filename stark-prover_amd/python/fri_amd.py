@@ -114,6 +114,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "fri_reset_profile": (i32, [vp]),
         "fri_debug_inject_stall": (i32, [vp, i32]),
+        "fri_debug_plan_layout": (i32, [sz, u32, u32, u32, ctypes.POINTER(ctypes.c_uint64), sz]),
         "fri_ctx_device_bytes": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "fri_debug_stamps": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), sz]),
         "fri_dist_unique_id": (i32, [ctypes.c_char_p]),
@@ -463,6 +464,23 @@ class Context:
         cur, peak = ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self.lib.fri_ctx_device_bytes(self.h, ctypes.byref(cur), ctypes.byref(peak)))
         return cur.value, peak.value
+
+
+def plan_layout(d: int, log_n: int, world: int = 1, rank: int = 0) -> dict:
+    """The commit plan's layout (fri_debug_plan_layout; host only, no GPU):
+    rounds bound, last sharded layer, per-layer slot sizes, x^-1 slices and
+    the block the rank holds."""
+    cap = 4 + 5 * (MAX_ROUNDS + 1)
+    out = (ctypes.c_uint64 * cap)()
+    rc = load_library().fri_debug_plan_layout(d, log_n, world, rank, out, cap)
+    if rc != FRI_OK:
+        raise FriError(rc, "fri_debug_plan_layout")
+    rmax = int(out[0])
+    layers = [dict(zip(("layer_words", "tree_words", "xinv_count", "xinv_start", "block"),
+                       (int(x) for x in out[4 + 5 * k: 9 + 5 * k]))) for k in range(rmax + 1)]
+    k_sw = int(out[1])
+    return {"rmax": rmax, "k_sw": k_sw - (1 << 64) if k_sw >= 1 << 63 else k_sw, "bytes": int(out[2]),
+            "layers": layers}
 
 
 # ----------------------------------------------------------------------------
