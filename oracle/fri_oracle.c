@@ -104,6 +104,16 @@ uint64_t orc_poly_evaluate(const uint64_t* c, size_t len, uint64_t x, uint64_t M
     return r;
 }
 
+/* Timing helper of bench.py's configs[0] leg (benches/poly_ops.rs:161-181
+ * shape): `reps` evaluations at x, x+1, ... in one call, so the per-call cost
+ * of the caller's FFI is not part of the figure; returns the sum of the
+ * values so the work stays live. */
+uint64_t orc_bench_evaluate(const uint64_t* c, size_t len, uint64_t x, uint64_t M, size_t reps) {
+    uint64_t acc = 0;
+    for (size_t k = 0; k < reps; k++) acc += orc_poly_evaluate(c, len, (x + k) % M, M);
+    return acc;
+}
+
 /* ops.rs:114-138  mul_assign (naive), result trimmed (update_degree).
  * out must hold la+lb-1 entries.  Returns trimmed length. */
 size_t orc_poly_mul(const uint64_t* a, size_t la, const uint64_t* b, size_t lb,

@@ -575,6 +575,8 @@ def load_c_oracle() -> ctypes.CDLL:
     lib.orc_poly_trim.argtypes = [p64, sz]
     lib.orc_poly_evaluate.restype = u64
     lib.orc_poly_evaluate.argtypes = [p64, sz, u64, u64]
+    lib.orc_bench_evaluate.restype = u64
+    lib.orc_bench_evaluate.argtypes = [p64, sz, u64, u64, sz]
     lib.orc_poly_mul.restype = sz
     lib.orc_poly_mul.argtypes = [p64, sz, p64, sz, p64, u64]
     lib.orc_poly_div_rem.restype = ctypes.c_int

@@ -1670,14 +1670,17 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         // ---- layer 0: coset LDE slice evals[rank + G*m] -------------------
         const uint32_t sft = mul_std(offset, pow_std(root_of_unity(log_n), rank));   // s = offset * w_n^rank
         sp = span_begin(ctx, "lde", d * 4 + M * 8);
-        launch_coset_coeffs(p.d_in, d, db.recv, M, pow_std(sft, M), s);              // P mod (x^M - s^M)
+        // P mod (x^M - s^M) has P's own coefficients when d <= M (blowup >= G):
+        // the NTT then reads the input directly (and skips its zero rows)
+        const bool fold_chunks = d > M;
+        if (fold_chunks) launch_coset_coeffs(p.d_in, d, db.recv, M, pow_std(sft, M), s);
         launch_pow_table(db.pre_lo, db.pre_hi, log_n - logG, sft, 1u, s);
         NttPlan np{};
         np.log_n = log_n - logG;
         np.tw = ctx->tw_fwd;
         np.pre_lo = db.pre_lo;
         np.pre_hi = db.pre_hi;
-        launch_ntt(np, db.recv, M, db.cyc, s);
+        launch_ntt(np, fold_chunks ? db.recv : p.d_in, fold_chunks ? M : d, db.cyc, s);
         span_end(ctx, sp);
         sp = span_begin(ctx, "alltoall", M * 4);
         rc = tp_alltoall(ctx, db.cyc, db.recv, (M / G) * 4, s);                       // coset slices -> blocks
