@@ -468,14 +468,14 @@ __device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[4], u
 #pragma unroll
         for (int i = 0; i < 4; i++) X[i] = R.iv[i];
     } else if (j == 3 || j == 4) {
-        Dg r;
-        dg_lds_load(root_lds, r);
-        const bool hi = (j == 4);
+        // one root byte per lane (lanes 0..15: this block's 16 bytes), its
+        // hex(hex()) word computed once, then read out as the 16 wave-uniform
+        // message words: 1 + 16 instructions instead of 16 per-word encodings
+        const uint32_t b = (__lane_id() & 15u) + (j == 4 ? 16u : 0u);
+        const uint32_t rw = reinterpret_cast<const uint32_t*>(root_lds)[b >> 2];
+        const uint32_t hh = hexhex((rw >> (24 - 8 * (b & 3))) & 255u);
 #pragma unroll
-        for (int jj = 0; jj < 16; jj++) {
-            const uint32_t rw = hi ? r.w[4 + (jj >> 2)] : r.w[jj >> 2];
-            w[jj] = hexhex((rw >> (24 - 8 * (jj & 3))) & 255u);
-        }
+        for (int jj = 0; jj < 16; jj++) w[jj] = __builtin_amdgcn_readlane(hh, jj);
         if (j == 3 && !has) {
 #pragma unroll
             for (int i = 0; i < 4; i++) X[i] = R.iv[i];
@@ -500,16 +500,22 @@ __device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[4], u
     }
 }
 
-// channel.rs:47-72: beta = U256(state) mod p  (the rehash is deferred)
+// channel.rs:47-72: beta = U256(state) mod p  (the rehash is deferred).
+// U256(state) = sum_i s_i 2^(32 (7-i)): eight independent products with the
+// Montgomery weights 2^(32 (8-i)) mod p and a sum tree, instead of eight
+// dependent Horner steps on the critical path after the root.
+constexpr uint32_t pow2_32k_mod_p(int k) {
+    uint64_t r = 1;
+    for (int j = 0; j < k; j++) r = (r << 32) % P;
+    return (uint32_t)r;
+}
 __device__ __forceinline__ uint32_t chan_beta(const uint32_t s[8]) {
-    uint32_t r = 0;
-    #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        // r <- (r * 2^32 + w_i) mod p:  redc(r * R^2) = r * 2^32 mod p
-        const uint32_t wi = s[i];
-        r = add(redc((uint64_t)r * R2_MOD_P), wi >= P ? wi - P : wi);
-    }
-    return r;
+    constexpr uint32_t W[8] = {pow2_32k_mod_p(8), pow2_32k_mod_p(7), pow2_32k_mod_p(6), pow2_32k_mod_p(5),
+                               pow2_32k_mod_p(4), pow2_32k_mod_p(3), pow2_32k_mod_p(2), pow2_32k_mod_p(1)};
+    uint32_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) t[i] = mmul(s[i] >= P ? s[i] - P : s[i], W[i]);
+    return add(add(add(t[0], t[1]), add(t[2], t[3])), add(add(t[4], t[5]), add(t[6], t[7])));
 }
 
 // ---------------------------------------------------------------- top ----
@@ -532,13 +538,16 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     const bool chan_wave = COMMIT && tid >= 448;
     DevState* st = t.st;
     uint32_t cs[8], X[4];
-    uint32_t has = 0;
+    uint32_t has = 0, forced = 0, fbeta = 0;
     int job = CJ_END_FINAL;
     if (chan_wave) {
 #pragma unroll
         for (int i = 0; i < 8; i++) cs[i] = st->chan[i];
         has = st->chan_has;
         job = !has ? CJ_ROOT : (st->chan_pending ? CJ_REHASH : CJ_MID);
+        // the test hook's beta, loaded now rather than after the root
+        forced = COMMIT ? st->forced : 0u;
+        if (forced && t.k < MAXR) fbeta = st->forced_beta[t.k];
     }
     // wave 6 pulls the compact-SHA constant tables into the scalar cache
     // while the inputs load (cold misses inside level 1 and the channel otherwise)
@@ -672,7 +681,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         for (int i = 0; i < 8; i++) st->chan[i] = cs[i];
         st->chan_has = 1;
         st->chan_pending = 1;                        // receive's rehash deferred to the next top
-        if (st->forced) beta = st->forced_beta[k];
+        if (forced) beta = fbeta;
         st->beta[k] = beta;
         st->beta_mont[k] = to_mont(beta);
         st->active[k] = 1;
@@ -714,6 +723,7 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
     __shared__ int32_t red[24];
     __shared__ uint32_t s_beta_m, s_active;
     __shared__ int32_t s_deg;
+    __shared__ uint32_t s_fbeta[TAIL_LOG + 2];   // the test hook's betas of these layers (0: not forced)
     const uint32_t tid = threadIdx.x;
     const bool chan_wave = tid >= 448;
     DevState* st = t0.st;
@@ -726,6 +736,11 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
     }
     uint32_t pending = chan_wave ? st->chan_pending : 0u;
     if (tid >= 384 && tid < 448) kcache_touch_sha_tables();
+    // forced betas (test hook) read here, off the per-layer critical path
+    if (tid < tt.n + 1) {
+        const int kk = t0.k + (int)tid;
+        s_fbeta[tid] = (st->forced && kk < MAXR) ? st->forced_beta[kk] + 1u : 0u;   // +1: 0 means not forced
+    }
     uint32_t beta_m = FOLD0 ? st->beta_mont[t0.k - 1] : 0u;
     int prev_deg = FOLD0 ? st->deg[t0.k - 1] : -1;
     const shaq::Role R = shaq::role_of(tid);
@@ -846,7 +861,7 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
                 for (int i = 0; i < 8; i++) st->chan[i] = cs[i];
                 st->chan_has = 1;
                 st->chan_pending = 1;                    // receive's rehash deferred to the next layer
-                if (st->forced) beta = st->forced_beta[k];
+                if (s_fbeta[li]) beta = s_fbeta[li] - 1u;
                 st->beta[k] = beta;
                 bm = to_mont(beta);
                 st->beta_mont[k] = bm;
