@@ -291,7 +291,15 @@ __global__ __launch_bounds__(TPB) void k_ntt_first_wide(const uint32_t* src, siz
     __shared__ uint32_t tws[P];                    // tw[0 .. 2^NS): w_{2^(t+1)}^j at 2^t + j
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < P; i += TPB) tws[i] = tw[i];
-    const size_t col0 = (size_t)blockIdx.x * C;
+    // Neighbouring tiles read neighbouring C-word pieces of the same input
+    // lines (8..64 bytes of each 128-byte line).  Blocks are dealt round-robin
+    // over the 8 XCDs (MI355X_MICROARCH.md "Workgroup dispatch"), each with its
+    // own L2: consecutive tiles go to blocks b, b + 8, b + 16, ... so that the
+    // tiles sharing a line run on one XCD, close in time, and the line is
+    // fetched from HBM once instead of once per XCD.
+    const uint32_t nb = gridDim.x;
+    const uint32_t tile = (nb & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
+    const size_t col0 = (size_t)tile * C;
     const uint32_t cbits = log_n - NS;
     // ---- load: rows q = q' 2^Z (the others are zero), VW words per lane ----
     constexpr uint32_t NV = (P >> Z) * VPR;
