@@ -288,6 +288,15 @@ int fri_commit_sharded_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, 
                               uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                               const uint32_t* forced_betas, fri_commit_result* out);
 
+/* Decommitment of one query after fri_commit_sharded (decommit_fri_layers,
+ * src/fri/fri_commit.rs:137-163), same layout and bytes as fri_decommit_query
+ * on a 1-GPU commit of the same codeword.  Collective: every rank calls it
+ * with the same index (the reference draws it from the transcript, identical
+ * on every rank) and receives the whole decommitment; each rank contributes
+ * the openings that lie in the blocks it holds. */
+int fri_decommit_query_sharded(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap,
+                               uint8_t* paths, size_t paths_cap, size_t* paths_len);
+
 /* ------------------------------------------------------------ diagnostics */
 /* Per-span device time (ms) accumulated while profiling is enabled (hipEvents
  * recorded on the context's stream; profiling commits run eagerly, no graph).

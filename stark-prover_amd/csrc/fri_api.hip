@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -83,6 +84,7 @@ struct DistBuf {
     uint32_t* pre_hi = nullptr;
     size_t gcap = 0;            // words in gath
     uint32_t* gath = nullptr;   // all-gathered layer at the switch to local
+    uint32_t* dq = nullptr;     // sharded decommitment: this rank's openings + all ranks' (G + 1 slots)
 };
 
 // One timed launch group: events recorded around it on the context stream.
@@ -278,6 +280,7 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     fri_dist_detach(ctx);
     dfree(ctx, ctx->db.cyc); dfree(ctx, ctx->db.recv); dfree(ctx, ctx->db.half); dfree(ctx, ctx->db.roots);
     dfree(ctx, ctx->db.top); dfree(ctx, ctx->db.pre_lo); dfree(ctx, ctx->db.pre_hi); dfree(ctx, ctx->db.gath);
+    dfree(ctx, ctx->db.dq);
     if (ctx->xstream) hipStreamDestroy(ctx->xstream);
     if (ctx->ev_vals) hipEventDestroy(ctx->ev_vals);
     if (ctx->ev_xchg) hipEventDestroy(ctx->ev_xchg);
@@ -1839,6 +1842,71 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     digest_to_bytes(h->chan, out->channel_out.digest);
     out->channel_out.has_state = h->chan_has;
     ctx->err.clear();
+    return FRI_OK;
+}
+
+// decommit_fri_layers (fri_commit.rs:137-163) after a sharded commit: the
+// opened elements of a sharded layer live in one rank's block (value and the
+// lower levels of the path in its block-local tree; the top log G levels in
+// the replicated top tree).  Every rank gathers the openings it holds and
+// zeros elsewhere (k_decommit_gather), the G outputs are all-gathered and
+// combined by a word-wise max (exactly one rank holds each non-zero word; the
+// replicated local layers are equal everywhere).  Collective: every rank
+// calls it with the same index and gets the same bytes, which equal
+// fri_decommit_query's for a 1-GPU commit of the same codeword.
+extern "C" int fri_decommit_query_sharded(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap,
+                                          uint8_t* paths, size_t paths_cap, size_t* paths_len) {
+    if (!ctx || !values || !paths_len) return fail(ctx, FRI_EINVAL, "null argument");
+    const Plan& p = ctx->plan;
+    if (!p.valid || ctx->h_state->n_layers == 0) return fail(ctx, FRI_ESTATE, "no committed layers");
+    if (!ctx->sharded_layers || !p.sharded) return fail(ctx, FRI_ESTATE, "last commit was not sharded: use fri_decommit_query");
+    if (!ctx->tp.host && !ctx->tp.comm) return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
+    const uint32_t G = p.G;
+    if ((uint32_t)ctx->tp.world != G) return fail(ctx, FRI_ESTATE, "transport world differs from the commit's");
+    uint32_t logG = 0;
+    while ((1u << logG) < G) logG++;
+    DecommitPlan dp{};
+    dp.index = index;
+    dp.log_n = p.log_n;
+    dp.n_layers = ctx->h_state->n_layers;
+    dp.logG = logG;
+    const bool local_tail = p.k_sw < p.rmax;
+    uint32_t words = 0;
+    for (uint32_t k = 0; k < dp.n_layers; k++) {
+        dp.layer_off[k] = p.layer_off[k];
+        dp.tree_off[k] = p.tree_off[k];
+        dp.path_off[k] = words;
+        words += 16 * (p.log_n - k);
+        if (k < ctx->sharded_layers) {
+            dp.shard_lb1[k] = (uint8_t)(p.log_n - k - logG + 1);
+            dp.val_block[k] = ((int)k == p.k_sw && local_tail) ? 0 : 1;   // the switch layer's slot was gathered whole
+            dp.owned[k] = (uint64_t)1 << p.block[k];
+            dp.top_off[k] = (uint64_t)k * 2 * 64 * 8;
+        }
+    }
+    *paths_len = (size_t)words * 4;
+    if (values_cap < 2 * (size_t)dp.n_layers) return fail(ctx, FRI_EINVAL, "values buffer too small (2 per layer)");
+    if (!paths || paths_cap < (size_t)words * 4) return fail(ctx, FRI_EINVAL, "paths buffer too small (see paths_len)");
+    const size_t tw = 2 * (size_t)dp.n_layers + words;
+    if (tw * 4 > 65536) return fail(ctx, FRI_EINVAL, "decommitment too large");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    DistBuf& db = ctx->db;
+    constexpr size_t SLOT = 16384;                          // words per rank slot (64 KiB)
+    if (!db.dq) FRI_HIP(ctx, dalloc(ctx, &db.dq, (size_t)(64 + 1) * SLOT * 4));
+    int rc = tp_host_stage(ctx, G * SLOT * 4);
+    if (rc) return rc;
+    hipStream_t s = ctx->stream;
+    launch_decommit_gather(p.layers, p.trees, dp, db.dq, s, db.top);
+    FRI_HIP(ctx, hipGetLastError());
+    if ((rc = tp_allgather(ctx, db.dq, db.dq + SLOT, SLOT * 4, s))) return rc;
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->tp.hs, db.dq + SLOT, G * SLOT * 4, hipMemcpyDeviceToHost, s));
+    if ((rc = sync_sharded(ctx, s))) return rc;
+    const uint32_t* all = reinterpret_cast<const uint32_t*>(ctx->tp.hs);
+    std::vector<uint32_t> o(tw, 0u);
+    for (uint32_t r = 0; r < G; r++)
+        for (size_t i = 0; i < tw; i++) o[i] = std::max(o[i], all[(size_t)r * SLOT + i]);
+    memcpy(values, o.data(), 2 * dp.n_layers * 4);
+    memcpy(paths, o.data() + 2 * dp.n_layers, (size_t)words * 4);
     return FRI_OK;
 }
 

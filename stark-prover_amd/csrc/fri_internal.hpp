@@ -91,9 +91,22 @@ struct DecommitPlan {
     uint64_t layer_off[MAXR + 1];
     uint64_t tree_off[MAXR + 1];
     uint32_t path_off[MAXR + 1];   // word offset of layer k's two paths (16 * L_j per earlier layer)
+    // Sharded layers (fri_decommit_query_sharded): layer k with shard_lb1[k] =
+    // log2(block size) + 1 (0: an ordinary whole layer) is held block-wise: this rank writes an opening
+    // only when it owns the opened element's block (owned[k], bit b), taking
+    // the path's lower log2(block) levels from its block-local tree and the
+    // top log G levels from the layer's top tree (top + top_off[k]); openings
+    // of blocks it does not hold are written as zeros (the ranks' outputs are
+    // then combined by a max-reduction).  val_block[k]: the value slot holds
+    // only this rank's block (index i mod B), else the whole layer (index i).
+    uint32_t logG;
+    uint8_t shard_lb1[MAXR + 1];    // log2(block size) + 1; 0: an ordinary (whole) layer
+    uint8_t val_block[MAXR + 1];
+    uint64_t owned[MAXR + 1];
+    uint64_t top_off[MAXR + 1];
 };
 void launch_decommit_gather(const uint32_t* layers, const uint32_t* trees, const DecommitPlan& dp, uint32_t* out,
-                            hipStream_t s);
+                            hipStream_t s, const uint32_t* top = nullptr);
 void launch_fold_plain(const uint32_t* in, uint32_t* out, uint32_t log_m, const uint32_t* xinv_m,
                        uint32_t beta, hipStream_t s);
 

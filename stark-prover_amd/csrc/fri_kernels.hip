@@ -850,15 +850,21 @@ void launch_fold_plain(const uint32_t* in, uint32_t* out, uint32_t log_m, const 
 // and the two authentication paths (sibling digest per level, leaf -> root),
 // as raw big-endian bytes.  One launch + one copy per query.
 __global__ void k_decommit_gather(const uint32_t* __restrict__ layers, const uint32_t* __restrict__ trees,
-                                  DecommitPlan dp, uint32_t* __restrict__ out) {
+                                  const uint32_t* __restrict__ top, DecommitPlan dp, uint32_t* __restrict__ out) {
     const uint32_t k = blockIdx.x;
     const uint32_t L = dp.log_n - k;
     const uint64_t m = (uint64_t)1 << L;
     const uint64_t idx = dp.index % m;
     const uint64_t sib = (idx + m / 2) % m;
+    const bool sharded = dp.shard_lb1[k] != 0;
+    const uint32_t lb = sharded ? dp.shard_lb1[k] - 1u : 0u;
+    const uint64_t bmask = sharded ? ((uint64_t)1 << lb) - 1 : ~(uint64_t)0;
+    // a sharded layer: is the opened element in a block this rank holds?
+    auto mine = [&](uint64_t i) -> bool { return !sharded || ((dp.owned[k] >> (i >> lb)) & 1u); };
+    auto vidx = [&](uint64_t i) -> uint64_t { return (sharded && dp.val_block[k]) ? (i & bmask) : i; };
     if (threadIdx.x == 0) {
-        out[2 * k] = layers[dp.layer_off[k] + idx];
-        out[2 * k + 1] = layers[dp.layer_off[k] + sib];
+        out[2 * k] = mine(idx) ? layers[dp.layer_off[k] + vidx(idx)] : 0u;
+        out[2 * k + 1] = mine(sib) ? layers[dp.layer_off[k] + vidx(sib)] : 0u;
     }
     const uint32_t l = threadIdx.x;
     if (l >= L) return;
@@ -867,15 +873,28 @@ __global__ void k_decommit_gather(const uint32_t* __restrict__ layers, const uin
 #pragma unroll
     for (int which = 0; which < 2; which++) {
         const uint64_t leaf = which ? sib : idx;
-        const uint32_t* d = tr + 8 * (level_offset(L, l) + ((leaf >> l) ^ 1u));
         uint32_t* o = paths + (size_t)which * 8 * L + 8 * l;
+        if (!mine(leaf)) {
+#pragma unroll
+            for (int w = 0; w < 8; w++) o[w] = 0u;
+            continue;
+        }
+        const uint32_t* d;
+        if (!sharded) {
+            d = tr + 8 * (level_offset(L, l) + ((leaf >> l) ^ 1u));
+        } else if (l < lb) {                         // inside the block: the block-local tree
+            d = tr + 8 * (level_offset(lb, l) + (((leaf & bmask) >> l) ^ 1u));
+        } else {                                     // above it: the replicated top tree of block roots
+            const uint32_t t = l - lb;
+            d = top + dp.top_off[k] + 8 * (level_offset(dp.logG, t) + (((leaf >> lb) >> t) ^ 1u));
+        }
 #pragma unroll
         for (int w = 0; w < 8; w++) o[w] = __builtin_bswap32(d[w]);
     }
 }
 void launch_decommit_gather(const uint32_t* layers, const uint32_t* trees, const DecommitPlan& dp, uint32_t* out,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(k_decommit_gather, dim3(dp.n_layers), dim3(64), 0, s, layers, trees, dp, out);
+                            hipStream_t s, const uint32_t* top) {
+    hipLaunchKernelGGL(k_decommit_gather, dim3(dp.n_layers), dim3(64), 0, s, layers, trees, top, dp, out);
 }
 
 }  // namespace fri

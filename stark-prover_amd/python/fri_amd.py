@@ -127,6 +127,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                      ctypes.POINTER(CommitResult)]),
         "fri_commit_sharded_device": (i32, [vp, vp, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
                                             ctypes.POINTER(CommitResult)]),
+        "fri_decommit_query_sharded": (i32, [vp, ctypes.c_uint64, pu32, sz, ctypes.c_char_p, sz,
+                                             ctypes.POINTER(sz)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -339,9 +341,12 @@ class Context:
         pl = 32 * depth
         return [(int(vals[j]), buf.raw[j * pl:(j + 1) * pl]) for j in range(count)]
 
-    def decommit_query(self, index: int, n_layers: int, log_n: int, generation: Optional[int] = None):
+    def decommit_query(self, index: int, n_layers: int, log_n: int, generation: Optional[int] = None,
+                       sharded: bool = False):
         """fri_decommit_query: per committed layer k, (value[idx], value[sib],
-        path(idx), path(sib)) with idx = index % m_k, sib = (idx + m_k/2) % m_k."""
+        path(idx), path(sib)) with idx = index % m_k, sib = (idx + m_k/2) % m_k.
+        sharded: after commit_sharded, fri_decommit_query_sharded (collective:
+        every rank calls it with the same index)."""
         self._resident(log_n, generation)
         if n_layers != self.commit_info()[2]:
             raise FriError(FRI_ESTATE, "layer count differs from the resident commit")
@@ -349,7 +354,8 @@ class Context:
         total = sum(64 * (log_n - k) for k in range(n_layers))
         buf = ctypes.create_string_buffer(max(total, 1))
         ln = ctypes.c_size_t()
-        self._check(self.lib.fri_decommit_query(self.h, index, _ptr(vals), vals.size, buf, total, ctypes.byref(ln)))
+        fn = self.lib.fri_decommit_query_sharded if sharded else self.lib.fri_decommit_query
+        self._check(fn(self.h, index, _ptr(vals), vals.size, buf, total, ctypes.byref(ln)))
         out, off = [], 0
         for k in range(n_layers):
             pl = 32 * (log_n - k)
@@ -544,6 +550,7 @@ class FRIProof:
     final_value: int
     final_degree: int
     generation: int = 0      # fri_commit_info generation of the commit that made it
+    sharded: bool = False    # made by fri_commit_sharded: decommitments are collective
 
     @property
     def n_layers(self) -> int:
@@ -568,7 +575,8 @@ def decommit_fri_layers(index: int, proof: "FRIProof", channel: Channel) -> None
     """src/fri/fri_commit.rs:137-163 over the device-resident layers/trees:
     per layer send value, path, sibling value, sibling path (a 1-element
     layer first sends its value, as the reference does)."""
-    for val, sval, path, spath in proof.ctx.decommit_query(index, proof.n_layers, proof.log_n, proof.generation):
+    for val, sval, path, spath in proof.ctx.decommit_query(index, proof.n_layers, proof.log_n, proof.generation,
+                                                           proof.sharded):
         # the gather reads layers of 2^(log_n-k) >= 2 elements; a 1-element
         # layer (blowup 1) has idx = sib = 0 and empty paths
         if not path and not spath:
@@ -840,6 +848,19 @@ def fri_commit(coeffs: Sequence[int], log_n: int, channel: Channel, offset: int 
     st = bytes.fromhex(channel.state) if channel.state else None
     res = ctx.commit(coeffs, log_n, offset, channel_state=st)
     return _mirror_commit(res, ctx, log_n, channel)
+
+
+def fri_commit_sharded(coeffs: Sequence[int], log_n: int, channel: Channel, ctx: Context,
+                       offset: int = GENERATOR) -> FRIProof:
+    """fri_commit (fri_commit.rs:72-122) over the ranks attached to ``ctx``
+    (one process per GPU, every rank passing the same coefficients and
+    channel): coset-sharded on the devices, the same transcript on every rank.
+    decommit_fri on the returned proof is collective (all ranks, same order)."""
+    st = bytes.fromhex(channel.state) if channel.state else None
+    res = ctx.commit_sharded(coeffs, log_n, offset, channel_state=st)
+    proof = _mirror_commit(res, ctx, log_n, channel)
+    proof.sharded = True
+    return proof
 
 
 def _mirror_commit(res: CommitResult, ctx: Context, log_n: int, channel: Channel) -> FRIProof:

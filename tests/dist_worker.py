@@ -56,6 +56,13 @@ def main():
             res["layer0_refused"] = True
         last = r.n_layers - 1
         res["last_layer_constant"] = bool((ctx.layer(last, log_n) == r.final_value).all())
+        # decommit_fri over the sharded proof (collective), then verify_fri on
+        # the whole transcript: paths to the roots, folds, final value
+        ch = fri_amd.Channel()
+        proof = fri_amd.fri_commit_sharded(coeffs, log_n, ch, ctx)
+        fri_amd.decommit_fri(3, (1 << log_n) - 1, proof, ch)
+        res["transcript_sha"] = __import__("hashlib").sha256(b"".join(ch.proof)).hexdigest()
+        res["verify_fri"] = bool(fri_amd.verify_fri(ch.proof, log_n, proof.n_layers, 3, (1 << log_n) - 1))
         print(f"[rank {rank}] 2^{log_n} sharded over {world}: {res['seconds']} s, HBM {peak / 2**30:.2f} GiB",
               file=sys.stderr, flush=True)
         ctx.detach()
@@ -83,8 +90,11 @@ def main():
         tail = ctx.layer(last, log_n)
         qi = min(1, tail.size - 1)            # a 1-element last layer (blowup 1) has only index 0
         _, path = ctx.auth_path(last, qi, log_n)
+        qidx = [0, 1, (1 << log_n) - 1, 0x9E3779B97F4A7C15 % (1 << log_n)]
+        dq_sharded = [ctx.decommit_query(i, r.n_layers, log_n, sharded=True) for i in qidx]
         ctx.detach()
         single = ctx.commit(coeffs, log_n)
+        res["decommit_matches_single"] = dq_sharded == [ctx.decommit_query(i, single.n_layers, log_n) for i in qidx]
         res["tail_matches_single"] = bool(np.array_equal(tail, ctx.layer(last, log_n)))
         res["auth_matches_single"] = path == ctx.auth_path(last, qi, log_n)[1]
         res["single_root0"] = bytes(single.roots[0]).hex()

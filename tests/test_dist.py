@@ -83,6 +83,7 @@ def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, corc, oracl
         assert r["final_value"] == ores.final_value
         assert r["state"] == och.state.decode()
         assert r["layer0_refused"] and r["tail_matches_single"] and r["auth_matches_single"]
+        assert r["decommit_matches_single"]
         assert r["single_root0"] == want_roots[0]
 
 
@@ -206,6 +207,7 @@ def test_sharded_2p28_world8_configs4(oracle_commit):
         assert r["final_value"] == want["final_value"] and r["final_degree"] == want["final_degree"]
         assert r["state"] == want["state"]
         assert r["layer0_refused"] and r["last_layer_constant"]
+        assert r["verify_fri"] and r["transcript_sha"] == got[0]["transcript_sha"]
         assert r["hbm_peak_bytes"] < 8 * 2**30, r["hbm_peak_bytes"]
     print("per-rank HBM (GiB):", [round(r["hbm_peak_bytes"] / 2**30, 2) for r in got])
 
@@ -224,5 +226,6 @@ def test_sharded_shard_sized_context(world, log_n, blowup_log, oracle_commit):
     for r in got:
         assert {k: r[k] for k in want} == want
         assert r["layer0_refused"] and r["last_layer_constant"]
+        assert r["verify_fri"] and r["transcript_sha"] == got[0]["transcript_sha"]
         d_bytes = 8 * ((1 << log_n) >> blowup_log)     # input + coefficient-fold buffers, full on every rank
         assert r["hbm_peak_bytes"] < 130 * (1 << log_n) / world + d_bytes + (512 << 20), r["hbm_peak_bytes"]
