@@ -1808,8 +1808,11 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
                 rc = local_tail();
                 hipGraph_t g = nullptr;
                 const hipError_t ec = hipStreamEndCapture(s, &g);
-                if (rc) return rc;
-                FRI_HIP(ctx, ec);
+                if (rc || ec != hipSuccess) {
+                    if (g) hipGraphDestroy(g);
+                    if (rc) return rc;
+                    FRI_HIP(ctx, ec);
+                }
                 p.tail_graph = g;
                 FRI_HIP(ctx, hipGraphInstantiate(&p.tail_exec, g, nullptr, nullptr, 0));
             }
