@@ -895,11 +895,20 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
         // are nodes of the graph: no host API call between the commits' kernels
         if (!p.exec) {
             FRI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-            FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
-            enqueue_commit(ctx);
-            FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
+            // a failure inside the capture still ends it (the stream must not
+            // stay in capture mode) and drops the partial graph
+            hipError_t e1 = hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s);
+            if (e1 == hipSuccess) enqueue_commit(ctx);
+            const hipError_t e2 = e1 == hipSuccess ? hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState),
+                                                                    hipMemcpyDeviceToHost, s)
+                                                   : e1;
             hipGraph_t g = nullptr;
-            FRI_HIP(ctx, hipStreamEndCapture(s, &g));
+            const hipError_t e3 = hipStreamEndCapture(s, &g);
+            if (e2 != hipSuccess || e3 != hipSuccess) {
+                if (g) hipGraphDestroy(g);
+                FRI_HIP(ctx, e2);
+                FRI_HIP(ctx, e3);
+            }
             p.graph = g;
             FRI_HIP(ctx, hipGraphInstantiate(&p.exec, g, nullptr, nullptr, 0));
         }
