@@ -56,6 +56,9 @@ __device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4) 
 #ifndef NTT_WIDE
 #define NTT_WIDE 1           // first pass of 9..12 stages instead of a 1..4-stage pass (k_ntt_first_wide)
 #endif
+#ifndef NTT_WIDE24
+#define NTT_WIDE24 0         // A/B: 2^24 in two 12-stage passes (k_ntt_later_wide12) instead of 8 + 8 + 8
+#endif
 
 // Z (FIRST only): the input has d <= n / 2^Z coefficients, so after the
 // bit-reversal gather every row q with q mod 2^Z != 0 is zero and DIT stages
@@ -433,6 +436,128 @@ __global__ __launch_bounds__(TPB) void k_ntt_first_wide(const uint32_t* src, siz
     }
 }
 
+// A later pass of 12 stages (k_ntt_later_wide12): the same 4 + 4 + 4 register
+// phases on a tile of 4096 rows x 2 columns, rows at stride 2^s0.  Each row
+// piece is 8 bytes, so the tiles sharing a 128-byte line are dealt to one XCD
+// (as in k_ntt_first_wide) and its L2 merges their reads and partial-line
+// writes.  Twiddles: small-table entry times one per-column factor, as in
+// k_ntt_pass; every element of a thread is in column tid / 256.
+template <int TPB>
+__global__ __launch_bounds__(TPB) void k_ntt_later_wide12(const uint32_t* src, uint32_t* dst, uint32_t log_n,
+                                                          uint32_t s0, const uint32_t* __restrict__ tw,
+                                                          const uint32_t* __restrict__ post_lo,
+                                                          const uint32_t* __restrict__ post_hi) {
+    constexpr uint32_t NS = 12, P = 1u << NS, TILE = 16u * TPB, C = TILE / P;
+    static_assert(C == 2 && TPB == 512, "4096 rows x 2 columns");
+    __shared__ uint32_t lds[TILE + TILE / 16 + 2 * (TILE >> 10)];
+    __shared__ uint32_t tws[P];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < P; i += TPB) tws[i] = tw[i];
+    const uint32_t nb = gridDim.x;
+    const uint32_t tile = (nb & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
+    const size_t col0 = (size_t)tile * C;
+    const size_t lomask = ((size_t)1 << s0) - 1;
+    auto gidx = [&](uint32_t q) -> size_t { return ((col0 >> s0) << (s0 + NS)) + ((size_t)q << s0) + (col0 & lomask); };
+    // ---- load: one 8-byte row piece per lane and step --------------------
+    uint2 v8[8];
+#pragma unroll
+    for (uint32_t r = 0; r < 8; r++) v8[r] = *reinterpret_cast<const uint2*>(src + gidx(r * TPB + tid));
+#pragma unroll
+    for (uint32_t r = 0; r < 8; r++) {
+        const uint32_t q = r * TPB + tid;
+        lds[ntt_laddr(q)] = v8[r].x;
+        lds[ntt_laddr(P + q)] = v8[r].y;
+    }
+    // column factor w_{2^(s+1)}^lo of stage s = s0 + t, by squarings from the top
+    uint32_t wl[NS];
+    {
+        const size_t lo = (col0 + (tid >> 8)) & lomask;
+        wl[NS - 1] = tw[((size_t)1 << (s0 + NS - 1)) + lo];
+#pragma unroll
+        for (int t = (int)NS - 2; t >= 0; t--) wl[t] = mmul(wl[t + 1], wl[t + 1]);
+    }
+    __syncthreads();
+    auto twid = [&](int t, uint32_t q0) -> uint32_t {
+        const uint32_t j = q0 & ((1u << t) - 1);
+        return j ? mmul(tws[(1u << t) + j], wl[t]) : wl[t];
+    };
+    uint32_t r[16];
+    // ---- phase 0: stages 0..3 on 16 consecutive rows ----------------------
+#pragma unroll
+    for (int e = 0; e < 16; e++) r[e] = lds[ntt_laddr(tid * 16 + e)];
+    {
+        const uint32_t x0 = tid * 16;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+                if (e & (1 << t)) continue;
+                const uint32_t u = r[e], v = mmul(r[e + (1 << t)], twid(t, (x0 + e) & (P - 1)));
+                r[e] = add(u, v);
+                r[e + (1 << t)] = sub(u, v);
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 16; e++) lds[ntt_laddr(tid * 16 + e)] = r[e];
+    __syncthreads();
+    // ---- phase 1: stages 4..7 -----------------------------------------------
+    {
+        const uint32_t ql = tid & 15, qh = (tid >> 4) & 15, c = tid >> 8;
+        const uint32_t base = c * P + ql + qh * 256;
+#pragma unroll
+        for (int m = 0; m < 16; m++) r[m] = lds[ntt_laddr(base + m * 16)];
+#pragma unroll
+        for (int t = 4; t < 8; t++) {
+            const int tb = t - 4;
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                if (m & (1 << tb)) continue;
+                const uint32_t u = r[m], v = mmul(r[m + (1 << tb)], twid(t, ql + ((uint32_t)m << 4)));
+                r[m] = add(u, v);
+                r[m + (1 << tb)] = sub(u, v);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++) lds[ntt_laddr(base + m * 16)] = r[m];
+    }
+    __syncthreads();
+    // ---- phase 2: stages 8..11, 16 rows at stride 256 -----------------------
+    {
+        const uint32_t c = tid >> 8, ql = tid & 255;
+#pragma unroll
+        for (int m = 0; m < 16; m++) r[m] = lds[ntt_laddr(c * P + ql + m * 256)];
+#pragma unroll
+        for (int t = 8; t < 12; t++) {
+            const int tb = t - 8;
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                if (m & (1 << tb)) continue;
+                const uint32_t u = r[m], v = mmul(r[m + (1 << tb)], twid(t, ql + ((uint32_t)m << 8)));
+                r[m] = add(u, v);
+                r[m + (1 << tb)] = sub(u, v);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++) lds[ntt_laddr(c * P + ql + m * 256)] = r[m];
+    }
+    __syncthreads();
+    // ---- store --------------------------------------------------------------
+#pragma unroll
+    for (uint32_t rr = 0; rr < 8; rr++) {
+        const uint32_t q = rr * TPB + tid;
+        uint32_t a = lds[ntt_laddr(q)], b = lds[ntt_laddr(P + q)];
+        const size_t g = gidx(q);
+        if (post_lo) {
+            a = pow2lvl(post_lo, post_hi, g, a);
+            b = pow2lvl(post_lo, post_hi, g + 1, b);
+        }
+        *reinterpret_cast<uint2*>(dst + g) = make_uint2(a, b);
+    }
+}
+
 template <int NS>
 static void launch_first_wide(const uint32_t* src, size_t d, uint32_t* dst, uint32_t log_n, const NttPlan& p,
                               bool last, uint32_t z, hipStream_t s) {
@@ -513,6 +638,17 @@ void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, 
     }
     uint32_t first = log_n % 8;
     if (first == 0) first = 8;
+#if NTT_WIDE24
+    // 2^24: two passes of 12 stages (k_ntt_first_wide<12> + k_ntt_later_wide12)
+    if (log_n == 24 && ((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
+        uint32_t z = 0;
+        while (z < 3 && ((size_t)d << (z + 1)) <= ((size_t)1 << log_n)) z++;
+        launch_first_wide<12>(src, d, dst, log_n, p, false, z, s);
+        hipLaunchKernelGGL((k_ntt_later_wide12<512>), dim3((unsigned)(((size_t)1 << log_n) / 8192)), dim3(512), 0, s,
+                           dst, dst, log_n, 12u, p.tw, p.post_lo, p.post_hi);
+        return;
+    }
+#endif
 #if NTT_WIDE
     // a short first pass (1..4 stages) merged with the next 8: one pass fewer
     if (first <= 4 && log_n >= 13 && log_n - first >= 8 &&

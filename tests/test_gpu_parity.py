@@ -58,7 +58,9 @@ def test_batch_inverse_edges(ctx):
                                      # first pass of 9..12 stages (k_ntt_first_wide) with 3, 2, 1 and 0
                                      # trivial stages, vectors straddling d, blowup 1
                                      (17, 1 << 14), (17, 16385), (18, 32767), (19, 1 << 16), (19, (1 << 19) - 1),
-                                     (20, 1 << 19), (20, 1 << 20), (21, 1 << 18), (23, 12345)])
+                                     (20, 1 << 19), (20, 1 << 20), (21, 1 << 18), (23, 12345),
+                                     # 2^24 with 2 and 0 trivial stages
+                                     (24, 1 << 22), (24, 1 << 24)])
 def test_lde_matches_oracle(ctx, corc, log_n, d):
     c = rng_field(log_n * 100 + d, d)
     got = ctx.lde(c, log_n, 5)
@@ -110,7 +112,7 @@ def test_evaluate_few_points_many_coefficients(ctx, corc, d, count):
 
 
 # ------------------------------------------------------ poly: interpolate --
-@pytest.mark.parametrize("log_n", [0, 1, 2, 5, 10, 13, 16, 17, 20])
+@pytest.mark.parametrize("log_n", [0, 1, 2, 5, 10, 13, 16, 17, 20, 24])
 def test_interpolate_roundtrip(ctx, corc, log_n):
     n = 1 << log_n
     c = rng_field(log_n + 5, n)
