@@ -317,6 +317,10 @@ __device__ __forceinline__ void reduce_mx(const int32_t* in, int32_t* out, uint3
     if (threadIdx.x == 0) { out[3 * w] = a; out[3 * w + 1] = b; out[3 * w + 2] = c; }
 }
 
+#ifndef MID_PAIR_BY_WG
+#define MID_PAIR_BY_WG 0     // 1: k_tree_mid<1024> levels 2-4 on lane pairs whatever the layer width (round-2 form)
+#endif
+
 // Mid tree: NIN level-l nodes per workgroup -> NIN/16 level-(l+4) nodes,
 // one node per lane per level.  NIN = 1024 (512 threads) for wide levels,
 // 256 (128 threads: one wave per SIMD on every level) for narrow ones.
@@ -349,7 +353,12 @@ __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L
     for (uint32_t j = 2; j <= 4; j++) {
         cnt >>= 1;
         uint32_t* out = tree + 8 * (level_offset(L, l + j) + (base >> j));
-        if (2 * cnt <= NIN / 2) {
+        // lane pairs only where the whole level is narrow: a lane-pair node
+        // issues 1744 instructions on two lanes, a per-lane node 2290 on one,
+        // and the wide instance's levels of >= 2^16 nodes are issue-bound
+        const bool narrow = NIN == 1024 && !MID_PAIR_BY_WG ? (size_t)cnt * gridDim.x < WIDE_PAIR_MAX
+                                                           : 2 * cnt <= NIN / 2;
+        if (narrow) {
             pair_level(A, B, out, t, cnt, qr);         // narrow: latency-bound
         } else if (t < cnt) {
             Dg a, b, o;
