@@ -187,7 +187,10 @@ int fri_trace_decommit(fri_ctx* ctx, uint64_t index, uint64_t stride, uint32_t c
  * beta = channel.receive_random_field_element(), fold; loop while the
  * folded polynomial's degree >= 1; channel.send(final.to_bytes()).
  * chan_in may be NULL (fresh Channel::new()).  Layers and trees stay on the
- * device until the next commit on this context. */
+ * device until the next commit on this context.  A coefficient >= p gives
+ * FRI_EINVAL: the device checks the coefficients in layer 0's coefficient
+ * scan, so the call returns only after the commit has run, with nothing
+ * served.  There is no host pass over the input. */
 int fri_commit(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n,
                uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                const uint32_t* forced_betas, fri_commit_result* out);

@@ -120,9 +120,14 @@ __device__ __forceinline__ int wave_max_i(int v) {
 __device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red /*LDS [3*waves]*/) {
     int m0 = -1, m1 = -1, m2 = -1;
     if (t.k == 0) {
+        // m1 >= 0 flags a coefficient >= p (the input is validated here, on
+        // the device, instead of by a host scan before the upload)
         const size_t n = t.d0, cs = (n + G - 1) / G, lo = (size_t)w * cs, hi = min(n, lo + cs);
-        for (size_t j = lo + threadIdx.x; j < hi; j += blockDim.x)
-            if (t.coef_in[j]) m0 = max(m0, (int)j);
+        for (size_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+            const uint32_t c = t.coef_in[j];
+            if (c) m0 = max(m0, (int)j);
+            if (c >= P) m1 = 0;
+        }
     } else {
         const DevState* st = t.st;
         const size_t len = (size_t)(st->deg[t.k - 1] + 1), nlen = (len + 1) / 2;
@@ -607,11 +612,13 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     lds_barrier();
     // ---- degree of poly_k (reference degree field; see DevState), uniform ----
     int deg = -1;
+    bool noncanon = false;                         // layer 0: an input coefficient >= p
     if (COMMIT) {
         int m0 = -1, m1 = -1, m2 = -1;
 #pragma unroll
         for (int i = 0; i < 8; i++) { m0 = max(m0, red[3 * i]); m1 = max(m1, red[3 * i + 1]); m2 = max(m2, red[3 * i + 2]); }
         deg = (t.k == 0) ? m0 : (m1 < 0 ? m2 : m0);
+        noncanon = t.k == 0 && m1 >= 0;
     }
     const bool is_final = COMMIT && deg < 1;
     const int job_end = is_final ? CJ_END_FINAL : CJ_END_ROUND;
@@ -677,6 +684,11 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     if (!COMMIT || tid != 448) return;
     // ---- results (wave 7, one lane) ----
     const int k = t.k;
+    if (noncanon) {                                // FRI_EINVAL: nothing of this commit is served
+        st->active[k] = 0;
+        st->status = 1u;
+        return;
+    }
     st->deg[k] = deg;
     Dg root;
     dg_lds_load(A, root);
@@ -789,8 +801,11 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
         // ---- coefficient fold of round k-1 (or the input scan at k == 0) ----
         int m0 = -1, m1 = -1, m2 = -1;
         if (k == 0) {
-            for (size_t j = tid; j < t.d0; j += blockDim.x)
-                if (t.coef_in[j]) m0 = max(m0, (int)j);
+            for (size_t j = tid; j < t.d0; j += blockDim.x) {
+                const uint32_t c = t.coef_in[j];
+                if (c) m0 = max(m0, (int)j);
+                if (c >= P) m1 = 0;                    // not canonical (see coef_task)
+            }
         } else {
             const uint32_t len = (uint32_t)(prev_deg + 1), nlen = (len + 1) / 2;
             const bool in_lds = li > 0 && k >= 2;      // poly_{k-1} was folded by this kernel
@@ -808,11 +823,13 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
         if ((tid & 63) == 0) { red[3 * (tid >> 6)] = m0; red[3 * (tid >> 6) + 1] = m1; red[3 * (tid >> 6) + 2] = m2; }
         lds_barrier();
         int deg;
+        bool noncanon;
         {
             int a = -1, b = -1, c = -1;
 #pragma unroll
             for (int i = 0; i < 8; i++) { a = max(a, red[3 * i]); b = max(b, red[3 * i + 1]); c = max(c, red[3 * i + 2]); }
             deg = (k == 0) ? a : (b < 0 ? c : a);
+            noncanon = k == 0 && b >= 0;
         }
         const bool is_final = deg < 1;
         const int job_end = is_final ? CJ_END_FINAL : CJ_END_ROUND;
@@ -856,7 +873,11 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
             if (level) { uint4* tmp = A; A = B; B = tmp; }
         }
         // ---- results (one lane of wave 7), hand-off to the next layer ----
-        if (tid == 448) {
+        if (tid == 448 && noncanon) {                   // FRI_EINVAL (uniform: the loop ends below)
+            st->active[k] = 0;
+            st->status = 1u;
+            s_active = 0;
+        } else if (tid == 448) {
             st->deg[k] = deg;
             Dg root;
             dg_lds_load(A, root);

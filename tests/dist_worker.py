@@ -75,8 +75,17 @@ def main():
         ctx = fri_amd.Context(0, log_n)
         ctx.attach_torch(rank, world)
         ctx.dist_selftest(1024)
+        # a coefficient >= p: rejected on the device by every rank (layer 0's
+        # replicated top), after the collectives ran in step on all ranks
+        bad = np.asarray(coeffs, dtype=np.uint32)
+        bad[len(bad) // 3] = fo.P
+        try:
+            ctx.commit_sharded(bad, log_n)
+            rejected = False
+        except fri_amd.FriError as e:
+            rejected = e.code == fri_amd.FRI_EINVAL
         r = ctx.commit_sharded(coeffs, log_n)
-        res = {"roots": [bytes(r.roots[k]).hex() for k in range(r.n_layers)],
+        res = {"noncanonical_rejected": rejected, "roots": [bytes(r.roots[k]).hex() for k in range(r.n_layers)],
                "betas": [int(r.betas[i]) for i in range(r.n_rounds)],
                "final_value": int(r.final_value), "final_degree": int(r.final_degree),
                "state": bytes(r.channel_out.digest).hex()}

@@ -84,6 +84,7 @@ def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, corc, oracl
         assert r["state"] == och.state.decode()
         assert r["layer0_refused"] and r["tail_matches_single"] and r["auth_matches_single"]
         assert r["decommit_matches_single"]
+        assert r["noncanonical_rejected"]
         assert r["single_root0"] == want_roots[0]
 
 

@@ -420,6 +420,38 @@ def _gpu_commit(ctx, coeffs, log_n):
             res.final_value, bytes(res.channel_out.digest).hex() if res.channel_out.has_state else "")
 
 
+@pytest.mark.parametrize("log_n", [5, 12, 16, 20])
+@pytest.mark.parametrize("where", ["first", "middle", "last"])
+def test_noncanonical_input_rejected_on_device(ctx, oracle, oracle_commit, log_n, where):
+    """The input coefficients are validated on the device, in layer 0's
+    coefficient scan (tail kernel at 2^5, wide leaf + top at 2^12/2^16, quad
+    leaf + mids + top at 2^20): a value >= p anywhere gives FRI_EINVAL, with
+    nothing served, through the host and the device entry points; the next
+    valid commit on the same context equals the C oracle's."""
+    import fri_amd
+    d = (1 << log_n) >> 3
+    seed = 500 + log_n
+    coeffs = oracle.splitmix64_np(seed, d).astype(np.uint32)
+    bad = coeffs.copy()
+    bad[{"first": 0, "middle": d // 2, "last": d - 1}[where]] = P if where != "middle" else 0xFFFFFFFF
+    with pytest.raises(fri_amd.FriError) as e:
+        ctx.commit(bad, log_n)
+    assert e.value.code == fri_amd.FRI_EINVAL
+    assert ctx.commit_info()[2] == 0                                    # no layers served
+    # the same input through fri_commit_device (the host call left it in the input buffer)
+    dptr = ctypes.c_void_p()
+    ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(dptr)))
+    res = fri_amd.CommitResult()
+    rc = ctx.lib.fri_commit_device(ctx.h, dptr, d, log_n, fri_amd.GENERATOR, None, 0, None, ctypes.byref(res))
+    assert rc == fri_amd.FRI_EINVAL
+    res = ctx.commit(coeffs, log_n)
+    got = {"roots": [bytes(res.roots[k]).hex() for k in range(res.n_layers)],
+           "betas": [int(res.betas[r]) for r in range(res.n_rounds)],
+           "final_value": int(res.final_value), "final_degree": int(res.final_degree),
+           "state": bytes(res.channel_out.digest).hex()}
+    assert got == oracle_commit(log_n, seed)
+
+
 @pytest.mark.parametrize("log_n,d", [(1, 1), (1, 2), (2, 1), (2, 4), (3, 3), (3, 8), (4, 16), (5, 7), (5, 32)])
 def test_tiny_codewords(ctx, oracle, log_n, d):
     """Smallest domains, including blowup 1 (d = n): the last layer has one element."""
