@@ -10,14 +10,16 @@ random polynomial with d = 2^21 coefficients (blowup 8) onto the codeword
 resident in HBM when the timed region starts, result (roots, betas, final
 value, channel state) read back to the host at the end of every step.
 
-N > 1 (torchrun, one process per GPU): weak scaling, 2^24 codeword elements
-per GPU.  Default --mode sharded: ONE codeword of 2^(24+log2 N) committed
-coset-sharded across the ranks (fri_commit_sharded_device over the library's
-RCCL communicator; BASELINE.json configs[4] at N=8 with --log-n 25).  The
-sharded transcript is checked against each rank's own 1-GPU commit before
-timing; on any mismatch/error every rank falls back to --mode replicas (N
-independent 2^24 commits) and the line carries a "note".  value = codeword
-elements committed per second by the whole job, timed by the slowest rank.
+N > 1 (torchrun, one process per GPU): by default strong scaling of ONE
+2^28 codeword (BASELINE.json configs[4]) committed coset-sharded across the
+ranks (fri_commit_sharded_device over the library's RCCL communicator), with
+the weak 2^24-per-GPU and the strong 2^24 points as secondary keys
+(`scaling_points`); `--log-n L` alone selects weak scaling, 2^L per GPU.
+The sharded transcript is checked against the C oracle's golden transcript
+(tests/golden/bench_transcripts.json) before timing; on any mismatch/error
+every rank falls back to --mode replicas (N independent commits) and
+`config.parallelism` says so.  value = codeword elements committed per second
+by the whole job, timed by the slowest rank.
 
 Prints ONE JSON line on rank 0.
 """
