@@ -268,6 +268,7 @@ int fri_dist_detach(fri_ctx* ctx);
 #define FRI_TRANSPORT_NONE 0
 #define FRI_TRANSPORT_RCCL 1
 #define FRI_TRANSPORT_HOST 2
+#define FRI_TRANSPORT_LOOPBACK 3   /* fri_debug_attach_loopback (timing rehearsal only) */
 int fri_dist_info(fri_ctx* ctx, int* rank, int* world, int* transport);
 /* Diagnostic: run the transport's all-to-all, all-gather and pair exchange
  * (both streams) on a known pattern and check the result; FRI_ERCCL with a
@@ -333,6 +334,13 @@ int fri_debug_plan_layout(size_t d, uint32_t log_n, uint32_t world, uint32_t ran
  * abort releases it.  The call then returns FRI_ERCCL and later sharded calls
  * FRI_ESTATE, exactly as for a real stall. */
 int fri_debug_inject_stall(fri_ctx* ctx, int enable);
+
+/* Timing rehearsal of one rank of a sharded commit on one device: attaches a
+ * transport whose collectives return this rank's own bytes, as device-to-
+ * device copies on the streams RCCL would use.  Every kernel of the rank runs
+ * on data of the right shape with no host round trip, but the transcript is
+ * not the real one (tools/shard_projection.py). */
+int fri_debug_attach_loopback(fri_ctx* ctx, int rank, int world);
 
 #ifdef __cplusplus
 }

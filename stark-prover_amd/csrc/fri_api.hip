@@ -66,6 +66,7 @@ struct Transport {
     ncclComm_t comm = nullptr;     // main stream collectives
     ncclComm_t xcomm = nullptr;    // exchange stream (separate communicator: no cross-stream ordering hazard)
     bool host = false;
+    bool loop = false;          // fri_debug_attach_loopback: every exchange returns this rank's own bytes
     fri_collectives ops{};
     uint8_t* hs = nullptr;      // pinned staging
     uint8_t* hr = nullptr;
@@ -1367,6 +1368,11 @@ static int sync_sharded(fri_ctx* ctx, hipStream_t s) {
 
 static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
     Transport& tp = ctx->tp;
+    if (tp.loop) {
+        for (int r = 0; r < tp.world; r++)
+            FRI_HIP(ctx, hipMemcpyAsync((uint8_t*)drecv + (size_t)r * bytes, dsend, bytes, hipMemcpyDeviceToDevice, s));
+        return FRI_OK;
+    }
     if (!tp.host) {
         FRI_NCCL(ctx, ncclAllGather(dsend, drecv, bytes, ncclUint8, tp.comm, s));
         return FRI_OK;
@@ -1382,6 +1388,10 @@ static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t byt
 
 static int tp_alltoall(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes_per_peer, hipStream_t s) {
     Transport& tp = ctx->tp;
+    if (tp.loop) {
+        FRI_HIP(ctx, hipMemcpyAsync(drecv, dsend, bytes_per_peer * tp.world, hipMemcpyDeviceToDevice, s));
+        return FRI_OK;
+    }
     if (!tp.host && ctx->inject_stall) {
         ctx->inject_stall = false;
         *ctx->stall_flag = 0u;
@@ -1411,6 +1421,10 @@ static int tp_alltoall(fri_ctx* ctx, const void* dsend, void* drecv, size_t byte
 
 static int tp_sendrecv(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, int peer, hipStream_t s) {
     Transport& tp = ctx->tp;
+    if (tp.loop) {
+        FRI_HIP(ctx, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, s));
+        return FRI_OK;
+    }
     if (!tp.host) {
         ncclComm_t c = (s == ctx->xstream) ? tp.xcomm : tp.comm;
         FRI_NCCL(ctx, ncclGroupStart());
@@ -1512,6 +1526,20 @@ extern "C" int fri_dist_attach_host(fri_ctx* ctx, int rank, int world, const fri
     return FRI_OK;
 }
 
+// Rehearsal transport for timing one rank's share of a sharded commit on one
+// device: collectives are device-to-device copies of this rank's own data on
+// the calling stream (the exchange stream included, as with RCCL), so the
+// GPU never waits for a host round trip.  The transcript is not the real one.
+extern "C" int fri_debug_attach_loopback(fri_ctx* ctx, int rank, int world) {
+    int rc = dist_check(ctx, rank, world);
+    if (rc) return rc;
+    fri_dist_detach(ctx);
+    ctx->tp.rank = rank;
+    ctx->tp.world = world;
+    ctx->tp.loop = true;
+    return FRI_OK;
+}
+
 extern "C" int fri_dist_detach(fri_ctx* ctx) {
     if (!ctx) return FRI_EINVAL;
     Transport& tp = ctx->tp;
@@ -1526,8 +1554,8 @@ extern "C" int fri_dist_detach(fri_ctx* ctx) {
 extern "C" int fri_dist_info(fri_ctx* ctx, int* rank, int* world, int* transport) {
     if (!ctx || !rank || !world || !transport) return fail(ctx, FRI_EINVAL, "null argument");
     const Transport& tp = ctx->tp;
-    if (tp.host) {
-        *transport = FRI_TRANSPORT_HOST;
+    if (tp.host || tp.loop) {
+        *transport = tp.host ? FRI_TRANSPORT_HOST : FRI_TRANSPORT_LOOPBACK;
         *rank = tp.rank;
         *world = tp.world;
     } else if (tp.comm) {
@@ -1641,7 +1669,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     while ((1u << logG) < G) logG++;
     if (G == 1 || log_n < SHARD_MIN_LOG || log_n < logG + 12)
         return run_commit(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
-    if (!ctx->tp.host && !ctx->tp.comm) return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
+    if (!ctx->tp.host && !ctx->tp.comm && !ctx->tp.loop) return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
     // a rank holds 1/G of the codeword: its NTT, twiddles and scratch are block-sized
     if (log_n - logG > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n - log2(world) out of range for context");
     const size_t n = (size_t)1 << log_n;
@@ -1880,7 +1908,7 @@ extern "C" int fri_decommit_query_sharded(fri_ctx* ctx, uint64_t index, uint32_t
     const Plan& p = ctx->plan;
     if (!p.valid || ctx->h_state->n_layers == 0) return fail(ctx, FRI_ESTATE, "no committed layers");
     if (!ctx->sharded_layers || !p.sharded) return fail(ctx, FRI_ESTATE, "last commit was not sharded: use fri_decommit_query");
-    if (!ctx->tp.host && !ctx->tp.comm) return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
+    if (!ctx->tp.host && !ctx->tp.comm && !ctx->tp.loop) return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
     const uint32_t G = p.G;
     if ((uint32_t)ctx->tp.world != G) return fail(ctx, FRI_ESTATE, "transport world differs from the commit's");
     uint32_t logG = 0;

@@ -114,6 +114,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "fri_reset_profile": (i32, [vp]),
         "fri_debug_inject_stall": (i32, [vp, i32]),
+        "fri_debug_attach_loopback": (i32, [vp, i32, i32]),
         "fri_debug_plan_layout": (i32, [sz, u32, u32, u32, ctypes.POINTER(ctypes.c_uint64), sz]),
         "fri_ctx_device_bytes": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "fri_debug_stamps": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), sz]),
@@ -423,15 +424,20 @@ class Context:
         self._cb = Collectives(None, t[1][1](allgather), t[2][1](alltoall), t[3][1](sendrecv))
         self._check(self.lib.fri_dist_attach_host(self.h, rank, world, ctypes.byref(self._cb)))
 
+    def attach_loopback(self, rank: int, world: int):
+        """Timing rehearsal (fri_debug_attach_loopback): collectives return
+        this rank's own bytes; the transcript is not the real one."""
+        self._check(self.lib.fri_debug_attach_loopback(self.h, rank, world))
+
     def detach(self):
         self._check(self.lib.fri_dist_detach(self.h))
 
     def dist_info(self):
         """(rank, world, transport) as the attached transport reports them
-        (transport: "none", "rccl" or "host"; fri_dist_info)."""
+        (transport: "none", "rccl", "host" or "loopback"; fri_dist_info)."""
         r, w, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         self._check(self.lib.fri_dist_info(self.h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(t)))
-        return r.value, w.value, ("none", "rccl", "host")[t.value]
+        return r.value, w.value, ("none", "rccl", "host", "loopback")[t.value]
 
     def dist_selftest(self, words_per_peer: int = 4096):
         self._check(self.lib.fri_dist_selftest(self.h, words_per_peer))
