@@ -89,6 +89,32 @@ def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, corc, oracl
 
 
 @pytest.mark.gpu
+def test_loopback_rehearsal_transport(oracle):
+    """fri_debug_attach_loopback (tools/shard_projection.py): one rank's share
+    of a sharded commit runs on one device with every round of the real
+    commit. The degree progression comes from the replicated coefficient fold,
+    so the layer and round counts equal the 1-GPU commit's. The roots are not
+    the real ones. Detaching ends the rehearsal."""
+    import fri_amd
+    import numpy as np
+    log_n, world = 22, 8
+    c = oracle.splitmix64_np(11, (1 << log_n) >> 3).astype(np.uint32)
+    ctx = fri_amd.Context(0, log_n - 3)
+    try:
+        ctx.attach_loopback(3, world)
+        assert ctx.dist_info() == (3, world, "loopback")
+        r = ctx.commit_sharded(c, log_n)
+        assert (r.n_layers, r.n_rounds) == (log_n - 2, log_n - 3)
+        ctx.detach()
+        assert ctx.dist_info()[2] == "none"
+        with pytest.raises(fri_amd.FriError) as e:
+            ctx.decommit_query(0, r.n_layers, log_n, sharded=True)
+        assert e.value.code == fri_amd.FRI_ESTATE
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
 def test_rccl_transport_selftest_world1():
     """The RCCL data path's calls (grouped send/recv all-to-all, all-gather,
     pair exchange on the split communicator + exchange stream) on the real
