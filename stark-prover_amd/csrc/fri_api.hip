@@ -1659,6 +1659,10 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
     return FRI_OK;
 }
 
+#ifndef SHARD_COEF_AFTER_LEAF
+#define SHARD_COEF_AFTER_LEAF 1
+#endif
+
 static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
                               uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                               const uint32_t* forced_betas, fri_commit_result* out) {
@@ -1788,13 +1792,22 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         if (Gc < 1) Gc = 1;
         if (Gc > 2048) Gc = 2048;
         const bool side = !ctx->profiling;   // (profiled commits keep one stream for the spans)
-        if (side) {
+        // The fold starts when the block tree's leaf kernel has ended, beside
+        // its latency-bound mids and top: next to the VALU-bound leaf kernel it
+        // took 4x longer and slowed the leaves (tools/shard_projection.py)
+        if (side && !SHARD_COEF_AFTER_LEAF) {
             FRI_HIP(ctx, hipEventRecord(ctx->ev_pre, s));
             FRI_HIP(ctx, hipStreamWaitEvent(ctx->cstream, ctx->ev_pre, 0));
             launch_coef(tc, Gc, ctx->cstream);
             FRI_HIP(ctx, hipEventRecord(ctx->ev_coef, ctx->cstream));
         }
-        launch_layer(tl, s, spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
+        launch_layer(tl, s, side && SHARD_COEF_AFTER_LEAF ? ctx->ev_pre
+                                                          : spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
+        if (side && SHARD_COEF_AFTER_LEAF) {
+            FRI_HIP(ctx, hipStreamWaitEvent(ctx->cstream, ctx->ev_pre, 0));
+            launch_coef(tc, Gc, ctx->cstream);
+            FRI_HIP(ctx, hipEventRecord(ctx->ev_coef, ctx->cstream));
+        }
         // all-gather block roots -> block order -> top tree level 0
         rc = tp_allgather(ctx, tl.tree + 8 * level_offset(tl.L, tl.L), db.roots, 32, s);
         if (rc) return rc;

@@ -33,14 +33,21 @@ void launch_coset_coeffs(const uint32_t* a, size_t d, uint32_t* out, size_t M, u
 }
 
 // block[G*t + r] = recv[r * (B/G) + t]
-__global__ void k_cyclic_to_block(const uint32_t* __restrict__ recv, uint32_t* __restrict__ block, size_t B, uint32_t G) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= B) return;
-    const size_t per = B / G;
-    block[i] = recv[(i % G) * per + i / G];
+// Thread j writes the G consecutive block words j*G .. j*G+G-1 as 16-byte
+// stores, reading word j of each of the G received slices (each read stream
+// coalesced across the wave).  G >= 4 (G = 2 takes the radix-2 path).
+__global__ void k_cyclic_to_block(const uint32_t* __restrict__ recv, uint32_t* __restrict__ block, size_t per,
+                                  uint32_t G) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= per) return;
+    uint4* out = reinterpret_cast<uint4*>(block + j * G);
+    for (uint32_t g = 0; g < G; g += 4)
+        out[g >> 2] = make_uint4(recv[g * per + j], recv[(g + 1) * per + j], recv[(g + 2) * per + j],
+                                 recv[(g + 3) * per + j]);
 }
 void launch_cyclic_to_block(const uint32_t* recv, uint32_t* block, size_t B, uint32_t G, hipStream_t s) {
-    hipLaunchKernelGGL(k_cyclic_to_block, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, recv, block, B, G);
+    const size_t per = B / G;
+    hipLaunchKernelGGL(k_cyclic_to_block, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, recv, block, per, G);
 }
 
 // out[j] = fold(first[j], second[j], xinv[j], beta_r), gated on active[r].
