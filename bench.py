@@ -406,6 +406,9 @@ def main():
     # The tree tops of one commit (one workgroup on the serial Fiat-Shamir
     # chain) overlap the leaf hashing of the others.  Beside `value`, never it.
     concurrent = None
+    pipelined = None
+    if world == 1 and mode == "single" and log_n >= 20:
+        pipelined = _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps=args.steps)
     if world == 1 and mode == "single" and log_n >= 20 and not args.no_extras:
         concurrent = _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C=3, steps=max(5, args.steps // 2))
 
@@ -462,6 +465,7 @@ def main():
             "pcie_inclusive": pcie,
             "decommit": decommit,
             "prover_trace_commit": trace_stage,
+            "pipelined_commits": pipelined,
             "concurrent_commits": concurrent,
             "prover_fibsq": prover,
             "cpu_baseline": cpu,
@@ -554,6 +558,33 @@ def _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C, steps):
     return {"commits_in_flight": C, "ms_per_commit": round(1000.0 * wall / (C * steps), 4),
             "value": round(C * steps * (1 << log_n) / wall, 1), "unit": "field-elems/s", "transcripts_ok": ok,
             "what": f"{C} host threads, one fri_ctx + stream each, {steps} commits of 2^{log_n} per thread"}
+
+
+def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps, depth=2):
+    """One context, one stream: commit k+1 is enqueued (fri_commit_device_async)
+    before commit k is collected (fri_commit_wait), so the device runs the
+    commits back to back without the host turnaround between them.  Every
+    collected transcript is compared with the first commit's."""
+    out = [fri_amd.CommitResult() for _ in range(steps)]
+
+    def run(k, results):
+        pend = []
+        for i in range(k):
+            pend.append(ctx.commit_device_async(dptr, d, log_n))
+            if len(pend) == depth:
+                ctx.commit_wait(pend.pop(0), results[i - depth + 1])
+        for j, t in enumerate(pend):
+            ctx.commit_wait(t, results[k - len(pend) + j])
+
+    run(depth, out)                                                  # warm-up: graphs of the slots
+    t0 = time.perf_counter()
+    run(steps, out)
+    wall = time.perf_counter() - t0
+    return {"depth": depth, "ms_per_commit": round(1000.0 * wall / steps, 4),
+            "value": round(steps * (1 << log_n) / wall, 1), "unit": "field-elems/s",
+            "transcripts_ok": all(_same(r, res0) for r in out),
+            "what": f"{steps} commits of 2^{log_n} on one fri_ctx, up to {depth} enqueued "
+                    "(fri_commit_device_async / fri_commit_wait): no host turnaround between commits"}
 
 
 def ctx_device(ctx):

@@ -205,6 +205,24 @@ int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t
  * reads without a copy.  Valid until fri_ctx_destroy. */
 int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
 
+/* Pipelined commits: a prover that commits many codewords in a row calls
+ * fri_commit (src/fri/fri_commit.rs:72-122) in a loop; here it enqueues them.
+ * fri_commit_device_async validates the arguments, enqueues the whole commit
+ * of fri_commit_device on the context stream and returns at once with a
+ * ticket; fri_commit_wait(ticket) waits for that commit and returns its
+ * result, with the same errors fri_commit_device would have returned.  Up to
+ * FRI_MAX_INFLIGHT commits may be pending (FRI_ESTATE beyond that).  They run
+ * one after another, so the device goes from one commit's last kernel to the
+ * next one's first with no host round trip in between.  A commit with another
+ * (d, log_n, offset) first waits for the pending ones.  The read-backs
+ * (fri_commit_info .. fri_decommit_query) serve the most recently enqueued
+ * commit and wait for it.  Not while profiling (FRI_ESTATE). */
+#define FRI_MAX_INFLIGHT 4
+int fri_commit_device_async(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
+                            uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                            const uint32_t* forced_betas, uint64_t* ticket);
+int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result* out);
+
 /* Which commit the read-backs below serve: `generation` grows with every
  * commit call on the context (successful or not), log_n / n_layers describe
  * the resident commit (n_layers = 0 when the last commit failed).  A binding

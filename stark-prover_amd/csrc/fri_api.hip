@@ -54,6 +54,8 @@ struct Plan {
     int32_t* wgmax = nullptr;       // per-workgroup coefficient maxima
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    hipGraph_t slot_graph[FRI_MAX_INFLIGHT] = {};       // fri_commit_device_async: one graph per result slot
+    hipGraphExec_t slot_exec[FRI_MAX_INFLIGHT] = {};    // (the DevState copy-out node targets the slot)
     hipGraph_t tail_graph = nullptr;        // sharded plan: the local layers after the switch
     hipGraphExec_t tail_exec = nullptr;
     bool graph_profiled = false;
@@ -106,7 +108,18 @@ struct fri_ctx {
     uint32_t* pow_lo = nullptr;
     uint32_t* pow_hi = nullptr;
     DevState* d_state = nullptr;
-    DevState* h_state = nullptr;    // pinned
+    DevState* h_state = nullptr;    // the state of the most recently enqueued commit (h_sync or a slot)
+    DevState* h_sync = nullptr;     // pinned: synchronous commits
+    // pipelined commits (fri_commit_device_async): pinned state per slot, an
+    // event after its copy-out, the ticket it holds and whether it is unwaited
+    DevState* h_slot[FRI_MAX_INFLIGHT] = {};
+    hipEvent_t ev_slot[FRI_MAX_INFLIGHT] = {};
+    uint64_t slot_ticket[FRI_MAX_INFLIGHT] = {};
+    uint32_t slot_log_n[FRI_MAX_INFLIGHT] = {};
+    bool slot_pending[FRI_MAX_INFLIGHT] = {};
+    bool slot_done[FRI_MAX_INFLIGHT] = {};  // the stream has passed the slot's event (settle)
+    uint64_t next_ticket = 1;
+    bool async_unsettled = false;   // commits enqueued since the stream was last drained
     Plan plan;
     bool profiling = false;
     std::map<std::string, ProfEntry> prof;
@@ -260,7 +273,8 @@ extern "C" int fri_ctx_create(int device, uint32_t log_n_max, fri_ctx** out) {
     CK(dalloc(ctx, &ctx->pow_lo, ((size_t)1 << POW_LO_LOG) * 4));
     CK(dalloc(ctx, &ctx->pow_hi, nhi * 4));
     CK(dalloc(ctx, &ctx->d_state, sizeof(DevState)));
-    CK(hipHostMalloc(&ctx->h_state, sizeof(DevState), hipHostMallocDefault));
+    CK(hipHostMalloc(&ctx->h_sync, sizeof(DevState), hipHostMallocDefault));
+    ctx->h_state = ctx->h_sync;
 #undef CK
     launch_twiddles(ctx->tw_fwd, log_n_max, false, ctx->stream);
     launch_twiddles(ctx->tw_inv, log_n_max, true, ctx->stream);
@@ -273,8 +287,13 @@ extern "C" int fri_dist_detach(fri_ctx* ctx);
 
 static void plan_free(fri_ctx* ctx) {
     Plan& p = ctx->plan;
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);   // pipelined commits may still use the plan
     if (p.exec) hipGraphExecDestroy(p.exec);
     if (p.graph) hipGraphDestroy(p.graph);
+    for (int i = 0; i < FRI_MAX_INFLIGHT; i++) {
+        if (p.slot_exec[i]) hipGraphExecDestroy(p.slot_exec[i]);
+        if (p.slot_graph[i]) hipGraphDestroy(p.slot_graph[i]);
+    }
     if (p.tail_exec) hipGraphExecDestroy(p.tail_exec);
     if (p.tail_graph) hipGraphDestroy(p.tail_graph);
     dfree(ctx, p.d_in); dfree(ctx, p.coefA); dfree(ctx, p.coefB); dfree(ctx, p.layers);
@@ -307,7 +326,11 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     if (ctx->interp_tmp) dfree(ctx, ctx->interp_tmp);
     dfree(ctx, ctx->trace_tree);
     dfree(ctx, ctx->trace_lde);
-    if (ctx->h_state) hipHostFree(ctx->h_state);
+    if (ctx->h_sync) hipHostFree(ctx->h_sync);
+    for (int i = 0; i < FRI_MAX_INFLIGHT; i++) {
+        if (ctx->h_slot[i]) hipHostFree(ctx->h_slot[i]);
+        if (ctx->ev_slot[i]) hipEventDestroy(ctx->ev_slot[i]);
+    }
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return FRI_OK;
@@ -856,9 +879,11 @@ static void enqueue_commit(fri_ctx* ctx) {
     }
 }
 
-static void init_state(fri_ctx* ctx, const fri_channel_state* chan_in, uint32_t flags,
+// Reset `h` (the pinned DevState a commit starts from and copies out to) and
+// make it the resident commit's state.
+static void init_state(fri_ctx* ctx, DevState* h, const fri_channel_state* chan_in, uint32_t flags,
                        const uint32_t* forced_betas) {
-    DevState* h = ctx->h_state;
+    ctx->h_state = h;
     memset(h, 0, sizeof(DevState));      // n_layers = 0: nothing readable until this commit succeeds
     ctx->commit_gen++;
     if (chan_in && chan_in->has_state) {
@@ -877,10 +902,21 @@ static void init_state(fri_ctx* ctx, const fri_channel_state* chan_in, uint32_t 
     }
 }
 
-static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
-                      uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
-                      const uint32_t* forced_betas, fri_commit_result* out) {
-    if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+// Pipelined commits may still be running: a call that reads the resident
+// commit (its pinned state, layers or trees) drains the stream first.
+static void settle(fri_ctx* ctx) {
+    if (!ctx->async_unsettled) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    ctx->async_unsettled = false;
+    if (ctx->h_state->status) ctx->h_state->n_layers = 0;   // a failed commit serves nothing
+}
+
+// Validate, build the plan and enqueue one commit on the context stream with
+// its DevState in `hs` (h_sync, or slot `slot` of the pipelined commits: each
+// slot replays its own graph, whose copy-out node targets that slot).
+static int commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
+                          uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                          const uint32_t* forced_betas, int slot) {
     if (log_n < 1 || log_n > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n out of range for context");
     const size_t n = (size_t)1 << log_n;
     if (d > n) return fail(ctx, FRI_EDEGREE, "more coefficients than domain points (domain would be exhausted)");
@@ -889,29 +925,32 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
     if (forced_betas && (flags & FRI_FLAG_FORCE_BETAS) && !check_canonical(forced_betas, MAXR))
         return fail(ctx, FRI_EINVAL, "forced beta not canonical");
     FRI_HIP(ctx, hipSetDevice(ctx->device));
-    int rc = plan_build(ctx, d, log_n, offset);
+    int rc = plan_build(ctx, d, log_n, offset);     // a new plan waits for the pending commits (plan_free)
     if (rc) return rc;
     Plan& p = ctx->plan;
     hipStream_t s = ctx->stream;
     ctx->sharded_layers = 0;
-    init_state(ctx, chan_in, flags, forced_betas);
+    DevState* hs = slot < 0 ? ctx->h_sync : ctx->h_slot[slot];
+    init_state(ctx, hs, chan_in, flags, forced_betas);
+    ctx->commit_log_n = log_n;
     if (host_coeffs && d)
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
     else if (dev_coeffs && dev_coeffs != p.d_in && d)
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, s));
     const bool use_graph = !(flags & FRI_FLAG_NO_GRAPH) && !ctx->profiling;
     if (use_graph) {
-        // the DevState copies in (from the pinned h_state just written) and out
+        // the DevState copies in (from the pinned state just written) and out
         // are nodes of the graph: no host API call between the commits' kernels
-        if (!p.exec) {
+        hipGraph_t& pg = slot < 0 ? p.graph : p.slot_graph[slot];
+        hipGraphExec_t& px = slot < 0 ? p.exec : p.slot_exec[slot];
+        if (!px) {
             FRI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             // a failure inside the capture still ends it (the stream must not
             // stay in capture mode) and drops the partial graph
-            hipError_t e1 = hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s);
+            hipError_t e1 = hipMemcpyAsync(ctx->d_state, hs, sizeof(DevState), hipMemcpyHostToDevice, s);
             if (e1 == hipSuccess) enqueue_commit(ctx);
-            const hipError_t e2 = e1 == hipSuccess ? hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState),
-                                                                    hipMemcpyDeviceToHost, s)
-                                                   : e1;
+            const hipError_t e2 =
+                e1 == hipSuccess ? hipMemcpyAsync(hs, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s) : e1;
             hipGraph_t g = nullptr;
             const hipError_t e3 = hipStreamEndCapture(s, &g);
             if (e2 != hipSuccess || e3 != hipSuccess) {
@@ -919,24 +958,25 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
                 FRI_HIP(ctx, e2);
                 FRI_HIP(ctx, e3);
             }
-            p.graph = g;
-            FRI_HIP(ctx, hipGraphInstantiate(&p.exec, g, nullptr, nullptr, 0));
+            pg = g;
+            FRI_HIP(ctx, hipGraphInstantiate(&px, g, nullptr, nullptr, 0));
         }
-        FRI_HIP(ctx, hipGraphLaunch(p.exec, s));
+        FRI_HIP(ctx, hipGraphLaunch(px, s));
     } else {
-        FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
+        FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, hs, sizeof(DevState), hipMemcpyHostToDevice, s));
         enqueue_commit(ctx);
         FRI_HIP(ctx, hipGetLastError());
-        FRI_HIP(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
+        FRI_HIP(ctx, hipMemcpyAsync(hs, ctx->d_state, sizeof(DevState), hipMemcpyDeviceToHost, s));
     }
-    FRI_HIP(ctx, hipStreamSynchronize(s));
-    if (ctx->profiling) spans_collect(ctx);
-    DevState* h = ctx->h_state;
+    return FRI_OK;
+}
+
+// The result of a finished commit from its copied-out DevState.
+static int commit_finish(fri_ctx* ctx, DevState* h, uint32_t log_n, fri_commit_result* out) {
     if (h->status) {
         h->n_layers = 0;                 // the failed commit's layers are not served by the read-backs
         return fail(ctx, (int)h->status, status_message(h->status));
     }
-    ctx->commit_log_n = log_n;
     memset(out, 0, sizeof *out);
     out->n_layers = h->n_layers;
     out->n_rounds = h->n_rounds;
@@ -949,6 +989,18 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
     out->channel_out.has_state = h->chan_has;
     ctx->err.clear();
     return FRI_OK;
+}
+
+static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
+                      uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                      const uint32_t* forced_betas, fri_commit_result* out) {
+    if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    int rc = commit_enqueue(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, -1);
+    if (rc) return rc;
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->async_unsettled = false;         // pending pipelined commits ran before this one
+    if (ctx->profiling) spans_collect(ctx);
+    return commit_finish(ctx, ctx->h_state, log_n, out);
 }
 
 extern "C" int fri_commit(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n, uint32_t offset,
@@ -965,6 +1017,44 @@ extern "C" int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t 
     return run_commit(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
 }
 
+extern "C" int fri_commit_device_async(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
+                                       uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                                       const uint32_t* forced_betas, uint64_t* ticket) {
+    if (!ctx || !ticket) return fail(ctx, FRI_EINVAL, "null argument");
+    if (d && !d_coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    if (ctx->profiling) return fail(ctx, FRI_ESTATE, "profiling: time commits with fri_commit_device");
+    int slot = -1;
+    for (int i = 0; i < FRI_MAX_INFLIGHT && slot < 0; i++)
+        if (!ctx->slot_pending[i]) slot = i;
+    if (slot < 0) return fail(ctx, FRI_ESTATE, "FRI_MAX_INFLIGHT commits pending: wait for one first");
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    if (!ctx->h_slot[slot]) {
+        FRI_HIP(ctx, hipHostMalloc(&ctx->h_slot[slot], sizeof(DevState), hipHostMallocDefault));
+        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_slot[slot], hipEventDisableTiming));
+    }
+    int rc = commit_enqueue(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, slot);
+    if (rc) return rc;
+    FRI_HIP(ctx, hipEventRecord(ctx->ev_slot[slot], ctx->stream));
+    ctx->slot_pending[slot] = true;
+    ctx->slot_ticket[slot] = ctx->next_ticket++;
+    ctx->slot_log_n[slot] = log_n;
+    ctx->async_unsettled = true;
+    *ticket = ctx->slot_ticket[slot];
+    return FRI_OK;
+}
+
+extern "C" int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result* out) {
+    if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    int slot = -1;
+    for (int i = 0; i < FRI_MAX_INFLIGHT && slot < 0; i++)
+        if (ctx->slot_pending[i] && ctx->slot_ticket[i] == ticket) slot = i;
+    if (slot < 0) return fail(ctx, FRI_EINVAL, "no pending commit with this ticket");
+    ctx->slot_pending[slot] = false;
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    FRI_HIP(ctx, hipEventSynchronize(ctx->ev_slot[slot]));
+    return commit_finish(ctx, ctx->h_slot[slot], ctx->slot_log_n[slot], out);
+}
+
 extern "C" int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr) {
     if (!ctx || !d_ptr) return fail(ctx, FRI_EINVAL, "null argument");
     // The plan's input buffer is only stable for a fixed (d, log_n, offset);
@@ -977,6 +1067,7 @@ extern "C" int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr) {
 
 extern "C" int fri_commit_info(fri_ctx* ctx, uint64_t* generation, uint32_t* log_n, uint32_t* n_layers) {
     if (!ctx || !generation || !log_n || !n_layers) return fail(ctx, FRI_EINVAL, "null argument");
+    settle(ctx);
     *generation = ctx->commit_gen;
     *n_layers = ctx->h_state->n_layers;
     *log_n = *n_layers ? ctx->commit_log_n : 0u;
@@ -985,6 +1076,7 @@ extern "C" int fri_commit_info(fri_ctx* ctx, uint64_t* generation, uint32_t* log
 
 extern "C" int fri_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out, size_t cap) {
     if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
     if (layer < ctx->sharded_layers)
@@ -997,6 +1089,7 @@ extern "C" int fri_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out, size_
 
 extern "C" int fri_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level, uint8_t* out, size_t cap) {
     if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
     if (layer < ctx->sharded_layers)
@@ -1021,6 +1114,7 @@ static int dq_alloc(fri_ctx* ctx);
 extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint32_t* value_out, uint8_t* path,
                              uint32_t* depth_out) {
     if (!ctx || !value_out || !depth_out) return fail(ctx, FRI_EINVAL, "null argument");
+    settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
     if (layer < ctx->sharded_layers)
@@ -1062,6 +1156,7 @@ static int dq_alloc(fri_ctx* ctx) {
 extern "C" int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap,
                                   uint8_t* paths, size_t paths_cap, size_t* paths_len) {
     if (!ctx || !values || !paths_len) return fail(ctx, FRI_EINVAL, "null argument");
+    settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || ctx->h_state->n_layers == 0) return fail(ctx, FRI_ESTATE, "no committed layers");
     if (ctx->sharded_layers)
@@ -1198,6 +1293,7 @@ extern "C" int fri_trace_decommit(fri_ctx* ctx, uint64_t index, uint64_t stride,
 // (100 MHz ticks), only in the -DFRI_STAMPS build.
 extern "C" int fri_debug_stamps(fri_ctx* ctx, uint64_t* out, size_t cap) {
     if (!ctx || !out) return FRI_EINVAL;
+    settle(ctx);
 #ifdef FRI_STAMPS
     const size_t n = sizeof(ctx->h_state->stamps) / sizeof(uint64_t);
     if (cap < n) return fail(ctx, FRI_EINVAL, "buffer too small");
@@ -1692,7 +1788,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     if (rc) return rc;
     DistBuf& db = ctx->db;
     ctx->sharded_layers = (uint32_t)p.rmax + 1;      // lowered when the tail goes local
-    init_state(ctx, chan_in, flags, forced_betas);
+    init_state(ctx, ctx->h_sync, chan_in, flags, forced_betas);
     FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
     if (host_coeffs && d)
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
@@ -1918,6 +2014,7 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
 extern "C" int fri_decommit_query_sharded(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap,
                                           uint8_t* paths, size_t paths_cap, size_t* paths_len) {
     if (!ctx || !values || !paths_len) return fail(ctx, FRI_EINVAL, "null argument");
+    settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || ctx->h_state->n_layers == 0) return fail(ctx, FRI_ESTATE, "no committed layers");
     if (!ctx->sharded_layers || !p.sharded) return fail(ctx, FRI_ESTATE, "last commit was not sharded: use fri_decommit_query");

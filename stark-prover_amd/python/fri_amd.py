@@ -37,6 +37,7 @@ HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "fri_a
 FRI_OK, FRI_EINVAL, FRI_ENOMEM, FRI_EHIP, FRI_ENODEV, FRI_ERCCL, FRI_ESTATE, FRI_EDEGREE = range(8)
 FLAG_FORCE_BETAS = 1
 FLAG_NO_GRAPH = 2
+MAX_INFLIGHT = 4          # FRI_MAX_INFLIGHT (fri_amd.h): pipelined commits pending per context
 
 
 class FriError(RuntimeError):
@@ -98,6 +99,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                              ctypes.POINTER(CommitResult)]),
         "fri_commit_device": (i32, [vp, vp, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
                                     ctypes.POINTER(CommitResult)]),
+        "fri_commit_device_async": (i32, [vp, vp, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
+                                          ctypes.POINTER(ctypes.c_uint64)]),
+        "fri_commit_wait": (i32, [vp, ctypes.c_uint64, ctypes.POINTER(CommitResult)]),
         "fri_ctx_input_buffer": (i32, [vp, sz, ctypes.POINTER(vp)]),
         "fri_commit_info": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "fri_layer_copy": (i32, [vp, u32, pu32, sz]),
@@ -254,6 +258,26 @@ class Context:
         res = CommitResult()
         self._check(self.lib.fri_commit(self.h, _ptr(c), c.size, log_n, offset, ctypes.byref(ch), flags,
                                         _ptr(fb) if fb is not None else None, ctypes.byref(res)))
+        return res
+
+    def commit_device_async(self, d_coeffs, d: int, log_n: int, offset: int = GENERATOR,
+                            channel_state: Optional[bytes] = None) -> int:
+        """Enqueue a commit of device-resident coefficients (``d_coeffs``: a
+        device pointer, e.g. from fri_ctx_input_buffer) and return its ticket
+        at once (fri_commit_device_async; at most MAX_INFLIGHT pending)."""
+        ch = ChannelState()
+        if channel_state:
+            ctypes.memmove(ch.digest, channel_state, 32)
+            ch.has_state = 1
+        t = ctypes.c_uint64()
+        self._check(self.lib.fri_commit_device_async(self.h, d_coeffs, d, log_n, offset, ctypes.byref(ch), 0, None,
+                                                     ctypes.byref(t)))
+        return t.value
+
+    def commit_wait(self, ticket: int, out: Optional[CommitResult] = None) -> CommitResult:
+        """Wait for an enqueued commit and return its result (fri_commit_wait)."""
+        res = out if out is not None else CommitResult()
+        self._check(self.lib.fri_commit_wait(self.h, ticket, ctypes.byref(res)))
         return res
 
     def commit_info(self):

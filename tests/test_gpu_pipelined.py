@@ -1,0 +1,147 @@
+"""Pipelined commits (fri_commit_device_async / fri_commit_wait): several
+commits of device-resident coefficients pending on one context, run back to
+back on its stream.  Each result must equal the C oracle's transcript of the
+same polynomial (fri_commit, src/fri/fri_commit.rs:72-122), whatever the
+order the tickets are collected in; read-backs serve the last enqueued commit;
+the limits and errors are those of include/fri_amd.h."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LOG_N = 16
+
+
+def _dev(torch, coeffs_u32):
+    """A device copy of the coefficients (torch owns the buffer)."""
+    return torch.from_numpy(coeffs_u32.view(np.int32).copy()).cuda()
+
+
+def _transcript(res):
+    return {"roots": [bytes(res.roots[k]).hex() for k in range(res.n_layers)],
+            "betas": [int(res.betas[r]) for r in range(res.n_rounds)],
+            "final_value": int(res.final_value), "final_degree": int(res.final_degree),
+            "state": bytes(res.channel_out.digest).hex()}
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    return t
+
+
+@pytest.fixture()
+def pctx():
+    import fri_amd
+    c = fri_amd.Context(0, LOG_N)
+    yield c
+    c.close()
+
+
+def _polys(oracle, torch, seeds, log_n=LOG_N):
+    d = (1 << log_n) >> 3
+    return [(s, _dev(torch, oracle.splitmix64_np(s, d).astype(np.uint32))) for s in seeds]
+
+
+def test_pipelined_results_match_oracle_any_order(pctx, oracle, oracle_commit, torch):
+    import fri_amd
+    d = (1 << LOG_N) >> 3
+    polys = _polys(oracle, torch, [901, 902, 903, 904])
+    tickets = [pctx.commit_device_async(buf.data_ptr(), d, LOG_N) for _, buf in polys]
+    assert len(set(tickets)) == fri_amd.MAX_INFLIGHT
+    for i in (2, 0, 3, 1):                                   # collected out of order
+        assert _transcript(pctx.commit_wait(tickets[i])) == oracle_commit(LOG_N, polys[i][0])
+    # the slots are free again: a second round through the same graphs
+    tickets = [pctx.commit_device_async(buf.data_ptr(), d, LOG_N) for _, buf in polys[::-1]]
+    for t, (seed, _) in zip(tickets, polys[::-1]):
+        assert _transcript(pctx.commit_wait(t)) == oracle_commit(LOG_N, seed)
+
+
+def test_pipelined_readbacks_serve_the_last_commit(pctx, oracle, oracle_commit, torch):
+    import hashlib
+    d = (1 << LOG_N) >> 3
+    polys = _polys(oracle, torch, [911, 912, 913])
+    g0 = pctx.commit_info()[0]
+    tickets = [pctx.commit_device_async(buf.data_ptr(), d, LOG_N) for _, buf in polys]
+    # before any wait: the read-backs wait for the stream and see the third commit
+    gen, log_n, n_layers = pctx.commit_info()
+    assert gen == g0 + 3 and log_n == LOG_N and n_layers == LOG_N - 2
+    last = oracle_commit(LOG_N, 913)
+    for k in (0, 5):
+        val, path = pctx.auth_path(k, 3, LOG_N)
+        h = hashlib.sha256(int(val).to_bytes(8, "big")).digest()
+        i = 3
+        for sib in path:
+            h = hashlib.sha256(h + sib if i % 2 == 0 else sib + h).digest()
+            i //= 2
+        assert h.hex() == last["roots"][k]
+    for t, (seed, _) in zip(tickets, polys):
+        assert _transcript(pctx.commit_wait(t)) == oracle_commit(LOG_N, seed)
+
+
+def test_pipelined_limits_and_errors(pctx, oracle, oracle_commit, torch):
+    import fri_amd
+    d = (1 << LOG_N) >> 3
+    (seed, buf), = _polys(oracle, torch, [921])
+    tickets = [pctx.commit_device_async(buf.data_ptr(), d, LOG_N) for _ in range(fri_amd.MAX_INFLIGHT)]
+    with pytest.raises(fri_amd.FriError) as e:               # FRI_MAX_INFLIGHT pending
+        pctx.commit_device_async(buf.data_ptr(), d, LOG_N)
+    assert e.value.code == fri_amd.FRI_ESTATE
+    with pytest.raises(fri_amd.FriError) as e:
+        pctx.commit_wait(max(tickets) + 1)                   # never issued
+    assert e.value.code == fri_amd.FRI_EINVAL
+    for t in tickets:
+        assert _transcript(pctx.commit_wait(t)) == oracle_commit(LOG_N, seed)
+    with pytest.raises(fri_amd.FriError) as e:
+        pctx.commit_wait(tickets[0])                         # already collected
+    assert e.value.code == fri_amd.FRI_EINVAL
+    pctx.set_profiling(True)
+    try:
+        with pytest.raises(fri_amd.FriError) as e:
+            pctx.commit_device_async(buf.data_ptr(), d, LOG_N)
+        assert e.value.code == fri_amd.FRI_ESTATE
+    finally:
+        pctx.set_profiling(False)
+    with pytest.raises(fri_amd.FriError) as e:
+        pctx.commit_device_async(buf.data_ptr(), (1 << LOG_N) + 1, LOG_N)   # d > n
+    assert e.value.code == fri_amd.FRI_EDEGREE
+
+
+def test_pipelined_noncanonical_input(pctx, oracle, oracle_commit, torch):
+    """A coefficient >= p fails that commit alone (FRI_EINVAL at its wait);
+    the commits before and after it in the pipeline are unaffected."""
+    import fri_amd
+    d = (1 << LOG_N) >> 3
+    good = oracle.splitmix64_np(931, d).astype(np.uint32)
+    bad = good.copy()
+    bad[d // 3] = 0xFFFFFFFF
+    gb, bb = _dev(torch, good), _dev(torch, bad)
+    t0 = pctx.commit_device_async(gb.data_ptr(), d, LOG_N)
+    t1 = pctx.commit_device_async(bb.data_ptr(), d, LOG_N)
+    assert pctx.commit_info()[2] == 0                        # the resident (last) commit failed
+    t2 = pctx.commit_device_async(gb.data_ptr(), d, LOG_N)
+    assert _transcript(pctx.commit_wait(t0)) == oracle_commit(LOG_N, 931)
+    with pytest.raises(fri_amd.FriError) as e:
+        pctx.commit_wait(t1)
+    assert e.value.code == fri_amd.FRI_EINVAL
+    assert _transcript(pctx.commit_wait(t2)) == oracle_commit(LOG_N, 931)
+    assert pctx.commit_info()[2] == LOG_N - 2
+
+
+def test_pipelined_with_plan_change_and_sync_commits(pctx, oracle, oracle_commit, torch):
+    """A commit with another (d, log_n) waits for the pending ones (their
+    results stay collectable); a synchronous commit in between too."""
+    d16 = (1 << LOG_N) >> 3
+    (s1, b1), (s2, b2) = _polys(oracle, torch, [941, 942])
+    (s3, b3), = _polys(oracle, torch, [943], log_n=14)
+    t1 = pctx.commit_device_async(b1.data_ptr(), d16, LOG_N)
+    t2 = pctx.commit_device_async(b2.data_ptr(), d16, LOG_N)
+    t3 = pctx.commit_device_async(b3.data_ptr(), (1 << 14) >> 3, 14)      # new plan
+    sync = pctx.commit(oracle.splitmix64_np(944, d16).astype(np.uint32), LOG_N)
+    assert _transcript(sync) == oracle_commit(LOG_N, 944)
+    assert _transcript(pctx.commit_wait(t3)) == oracle_commit(14, s3)
+    assert _transcript(pctx.commit_wait(t1)) == oracle_commit(LOG_N, s1)
+    assert _transcript(pctx.commit_wait(t2)) == oracle_commit(LOG_N, s2)
+    assert pctx.commit_info()[1:] == (LOG_N, LOG_N - 2)      # the sync commit is resident
