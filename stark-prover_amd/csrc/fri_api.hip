@@ -1982,24 +1982,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         return rc;
     }
     if (ctx->profiling) spans_collect(ctx);
-    DevState* h = ctx->h_state;
-    if (h->status) {
-        h->n_layers = 0;                 // the failed commit's layers are not served by the read-backs
-        return fail(ctx, (int)h->status, status_message(h->status));
-    }
     ctx->commit_log_n = log_n;
-    memset(out, 0, sizeof *out);
-    out->n_layers = h->n_layers;
-    out->n_rounds = h->n_rounds;
-    out->log_n = log_n;
-    out->final_value = h->final_value;
-    out->final_degree = h->final_degree;
-    for (uint32_t kk = 0; kk < h->n_layers && kk <= (uint32_t)MAXR; kk++) digest_to_bytes(h->roots[kk], out->roots[kk]);
-    for (uint32_t r = 0; r < h->n_rounds && r < (uint32_t)MAXR; r++) out->betas[r] = h->beta[r];
-    digest_to_bytes(h->chan, out->channel_out.digest);
-    out->channel_out.has_state = h->chan_has;
-    ctx->err.clear();
-    return FRI_OK;
+    return commit_finish(ctx, ctx->h_state, log_n, out);
 }
 
 // decommit_fri_layers (fri_commit.rs:137-163) after a sharded commit: the
