@@ -145,3 +145,60 @@ def test_pipelined_with_plan_change_and_sync_commits(pctx, oracle, oracle_commit
     assert _transcript(pctx.commit_wait(t1)) == oracle_commit(LOG_N, s1)
     assert _transcript(pctx.commit_wait(t2)) == oracle_commit(LOG_N, s2)
     assert pctx.commit_info()[1:] == (LOG_N, LOG_N - 2)      # the sync commit is resident
+
+
+def test_pipelined_channel_state_and_eager_flag(pctx, oracle, corc, torch):
+    """A channel state carried in (fri_commit's &mut Channel after earlier
+    sends) and the eager (no-graph) flag go through the pipelined entry point
+    too: each transcript equals the C oracle's from the same channel state."""
+    import fri_amd
+    d = (1 << LOG_N) >> 3
+    c = oracle.splitmix64_np(951, d).astype(np.uint32)
+    buf = _dev(torch, c)
+    state = bytes(range(32))
+    och = oracle.OrcChannel()                              # the C oracle's channel, state as hex
+    corc.orc_channel_init(ctypes.byref(och))
+    och.state = state.hex().encode()
+    och.state_len = 64
+    cs = np.ascontiguousarray(c.astype(np.uint64))
+    ores = oracle.OrcFriResult()
+    assert corc.orc_fri_commit_fast(cs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), d, LOG_N, 5, 5,
+                                    oracle.P, ctypes.byref(och), None, ctypes.byref(ores), None, None) == 0
+    want = {"roots": [bytes(ores.roots[k]).hex() for k in range(ores.n_layers)],
+            "betas": [int(ores.betas[r]) for r in range(ores.n_rounds)],
+            "final_value": int(ores.final_value), "final_degree": int(ores.final_degree),
+            "state": och.state.decode()}
+    assert _transcript(pctx.commit(c, LOG_N, channel_state=state)) == want
+    t0 = pctx.commit_device_async(buf.data_ptr(), d, LOG_N, channel_state=state)
+    ch = fri_amd.ChannelState()
+    ctypes.memmove(ch.digest, state, 32)
+    ch.has_state = 1
+    t1 = ctypes.c_uint64()
+    pctx._check(pctx.lib.fri_commit_device_async(pctx.h, buf.data_ptr(), d, LOG_N, fri_amd.GENERATOR,
+                                                 ctypes.byref(ch), fri_amd.FLAG_NO_GRAPH, None, ctypes.byref(t1)))
+    assert _transcript(pctx.commit_wait(t1.value)) == want
+    assert _transcript(pctx.commit_wait(t0)) == want
+
+
+def test_pipelined_then_sharded_on_one_context(oracle, oracle_commit, torch):
+    """Pending pipelined commits and a sharded commit (loopback rehearsal
+    transport, world 1 would not shard: world 2) on the same context: the
+    sharded plan waits for the pending commits, whose results stay
+    collectable; a 1-GPU pipelined commit afterwards is exact again."""
+    import fri_amd
+    log_n = 21
+    d = (1 << log_n) >> 3
+    cx = fri_amd.Context(0, log_n)
+    try:
+        c = oracle.splitmix64_np(961, d).astype(np.uint32)
+        buf = _dev(torch, c)
+        t = [cx.commit_device_async(buf.data_ptr(), d, log_n) for _ in range(2)]
+        cx.attach_loopback(0, 2)
+        cx.commit_sharded(c, log_n)          # loopback: not the real transcript, only the plan switch
+        cx.detach()
+        for ti in t:
+            assert _transcript(cx.commit_wait(ti)) == oracle_commit(log_n, 961)
+        t2 = cx.commit_device_async(buf.data_ptr(), d, log_n)
+        assert _transcript(cx.commit_wait(t2)) == oracle_commit(log_n, 961)
+    finally:
+        cx.close()
