@@ -377,6 +377,7 @@ extern "C" int fri_lde(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t 
     launch_pow_table(ctx->pow_lo, ctx->pow_hi, log_n, offset, 1u, ctx->stream);
     p.pre_lo = ctx->pow_lo;
     p.pre_hi = ctx->pow_hi;
+    p.scratch = ctx->scratch_c;
     launch_ntt(p, ctx->scratch_a, d, ctx->scratch_b, ctx->stream);
     FRI_HIP(ctx, hipGetLastError());
     FRI_HIP(ctx, hipMemcpyAsync(evals_out, ctx->scratch_b, n * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -840,6 +841,7 @@ static void enqueue_commit(fri_ctx* ctx) {
     NttPlan np = lde_plan(ctx, log_n);
     np.pre_lo = p.pre_lo;
     np.pre_hi = p.pre_hi;
+    np.scratch = p.trees;                 // free until layer 0's leaf kernel (>= 16n words)
     size_t sp = span_begin(ctx, "lde", p.d * 4 + n * 4);
     launch_ntt(np, p.d_in, p.d, p.layers + p.layer_off[0], s);
     span_end(ctx, sp);

@@ -59,6 +59,7 @@ struct NttPlan {
     const uint32_t* pre_hi;
     const uint32_t* post_lo;     // optional output scale t^j (Montgomery, two-level)
     const uint32_t* post_hi;
+    uint32_t* scratch;           // optional 2^log_n words the transform may use (2^24 coset LDE); else nullptr
 };
 // dst[k] = post(k) * sum_{j<d} src[j]*pre(j)*w^(jk); src may alias nothing in dst.
 void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, hipStream_t s);

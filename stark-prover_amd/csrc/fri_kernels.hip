@@ -56,6 +56,9 @@ __device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4) 
 #ifndef NTT_WIDE
 #define NTT_WIDE 1           // first pass of 9..12 stages instead of a 1..4-stage pass (k_ntt_first_wide)
 #endif
+#ifndef NTT_LDE24
+#define NTT_LDE24 0          // A/B: 2^24 LDE (d <= 2^21) as gather + two passes (k_lde24_*); measured slower
+#endif
 #ifndef NTT_WIDE24
 #define NTT_WIDE24 0         // A/B: 2^24 in two 12-stage passes (k_ntt_later_wide12) instead of 8 + 8 + 8
 #endif
@@ -69,7 +72,11 @@ __device__ __forceinline__ uint32_t ntt_laddr(uint32_t x) { return x + (x >> 4) 
 // words per lane as one 16-byte access, all four of a lane's accesses issued
 // before the first LDS write (or HBM store), instead of 16 4-byte accesses
 // issued four at a time.
-template <int A, int B, bool FIRST, int TPB, int Z = 0, bool VEC = false>
+// YSRC (the second pass of the 2^24 coset LDE, k_lde24_a): the source is the
+// coset-major array y[c][row][q] that k_lde24_a writes, element (row, column
+// lo) of this pass at y[lo mod 8][row][lo / 8]; tiles are dealt XCD-aware (the
+// eight tiles reading 16-byte pieces of the same y lines on one L2).
+template <int A, int B, bool FIRST, int TPB, int Z = 0, bool VEC = false, bool YSRC = false>
 __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d, uint32_t* dst,
                                                   uint32_t log_n, uint32_t s0, const uint32_t* __restrict__ tw,
                                                   const uint32_t* __restrict__ pre_lo, const uint32_t* __restrict__ pre_hi,
@@ -82,7 +89,9 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
     const uint32_t tid = threadIdx.x;
     if (NTT_TWS && tid < P) tws[tid] = tw[tid];
     const size_t ncols = ((size_t)1 << log_n) >> NS;
-    const size_t col0 = (size_t)blockIdx.x * C;
+    static_assert(!YSRC || (VEC && !FIRST && NS == 8 && C == 32), "coset source: later 8-stage vector pass");
+    const uint32_t nb = gridDim.x;
+    const size_t col0 = (size_t)(YSRC && !(nb & 7u) ? (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3) : blockIdx.x) * C;
     const size_t lomask = ((size_t)1 << s0) - 1;
     // FIRST (bit-reversed input): tile column c is output column
     // bitrev(col0 + c) over the log_n - NS column bits, so its row q reads
@@ -118,6 +127,11 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
                     v.z = pow2lvl(pre_lo, pre_hi, si + 2, v.z);
                     v.w = pow2lvl(pre_lo, pre_hi, si + 3, v.w);
                 }
+            } else if (YSRC) {
+                // lane: row q, coset cc; words lo = col0 + 8 i + cc, i < 4 (y[cc][q][col0/8 + i])
+                const size_t m8 = ((size_t)1 << log_n) >> 3;
+                const uint32_t cc = y & 7u, qq = y >> 3;
+                v = *reinterpret_cast<const uint4*>(src + cc * m8 + ((size_t)qq << (log_n - 3 - NS)) + (col0 >> 3));
             } else {
                 v = *reinterpret_cast<const uint4*>(src + gidx(c, q));
             }
@@ -126,6 +140,14 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(const uint32_t* src, size_t d,
 #pragma unroll
         for (uint32_t r = 0; r < 4; r++) {
             const uint32_t y = r * TPB + tid;
+            if (YSRC) {
+                const uint32_t cc = y & 7u, qq = y >> 3;
+                lds[ntt_laddr(cc * P + qq)] = v4[r].x;
+                lds[ntt_laddr((8 + cc) * P + qq)] = v4[r].y;
+                lds[ntt_laddr((16 + cc) * P + qq)] = v4[r].z;
+                lds[ntt_laddr((24 + cc) * P + qq)] = v4[r].w;
+                continue;
+            }
             const uint32_t c = (y % VPR) * 4, q = y / VPR;
             lds[ntt_laddr(c * P + q)] = v4[r].x;
             lds[ntt_laddr((c + 1) * P + q)] = v4[r].y;
@@ -558,6 +580,165 @@ __global__ __launch_bounds__(TPB) void k_ntt_later_wide12(const uint32_t* src, u
     }
 }
 
+// ---- 2^24 coset LDE in two passes (NTT_LDE24) ----------------------------
+// With d <= 2^21 = n/8 coefficients, the DIT's first three stages only copy
+// (the bit-reversed input is nonzero only at positions p = 0 mod 8), and the
+// positions p = 8q + c of one residue c never meet another residue's in a
+// later butterfly: stages 3..15 of the transform split into 8 independent
+// 13-stage transforms per 2^16-position column, one per coset class c
+// (eval[i], i = c mod 8, is P on the coset offset*w_n^c*<w_n^8>).  Stage
+// s = t + 3 of class c uses the twiddle w_{2^(t+4)}^(8 (q mod 2^t) + c) =
+// tw[2^(t+3) + 8 (q mod 2^t) + c].  So:
+//   k_lde24_gather  X[r][k] = coeff[256 r + k] * offset^(256 r + k), written
+//                   transposed: a0[col][r] = X[r][bitrev8(col)] (8 MB);
+//   k_lde24_a       one (column, class) per workgroup: the 2^13 values
+//                   X[bitrev13(q)][bitrev8(col)], 13 stages in LDS, written
+//                   contiguously to y[c][col][q] (32 KB per workgroup);
+//   k_ntt_pass<YSRC> stages 16..23 from y into the natural-order output:
+//                   rows of 32 consecutive words (128-byte lines).
+// Both passes write whole lines; the three-pass form reads and writes the
+// 64 MB codeword three times (8 + 8 + 8 stages).  Measured (kernel trace,
+// profiles/r03_lde24_kt.txt): gather 21.9 + pass A 72.5 + pass B 45.8 us
+// against 37.5 + 39.8 + 39.7 us for the three passes.  Both forms cost about
+// 5.6 us per real stage (21 either way): the passes are bound by butterfly
+// issue, not by their loads and stores, so the pass count is not the lever.
+// Off by default (-DNTT_LDE24=1 builds it; parity green).
+__global__ __launch_bounds__(256) void k_lde24_gather(const uint32_t* __restrict__ src, size_t d, uint32_t* __restrict__ a0,
+                                                      const uint32_t* __restrict__ pre_lo,
+                                                      const uint32_t* __restrict__ pre_hi) {
+    __shared__ uint32_t t[32][257];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t r0 = blockIdx.x * 32u;
+#pragma unroll 4
+    for (uint32_t i = 0; i < 32; i++) {                    // rows r0 + i: 1 KB each, coalesced
+        const size_t j = (size_t)(r0 + i) * 256u + tid;
+        uint32_t v = 0u;
+        if (j < d) {
+            v = src[j];
+            if (pre_lo) v = pow2lvl(pre_lo, pre_hi, j, v);
+        }
+        t[i][tid] = v;
+    }
+    __syncthreads();
+    // 256 output rows col of 32 words (r0 .. r0 + 31): 8 lanes x 16 bytes per row
+#pragma unroll
+    for (uint32_t it = 0; it < 8; it++) {
+        const uint32_t col = it * 32u + (tid >> 3), part = tid & 7u;
+        const uint32_t k = __brev(col) >> 24;
+        const uint4 w = make_uint4(t[4 * part][k], t[4 * part + 1][k], t[4 * part + 2][k], t[4 * part + 3][k]);
+        *reinterpret_cast<uint4*>(a0 + (size_t)col * 8192u + r0 + 4 * part) = w;
+    }
+}
+
+__global__ __launch_bounds__(512) void k_lde24_a(const uint32_t* __restrict__ a0, uint32_t* __restrict__ y,
+                                                 const uint32_t* __restrict__ tw) {
+    constexpr uint32_t P = 8192, TPB = 512;
+    __shared__ uint32_t lds[P + P / 16 + 2 * (P >> 10)];
+    __shared__ uint32_t twc[P];                  // twc[2^t + j] = w_{2^(t+4)}^(8 j + c), t < 13
+    const uint32_t tid = threadIdx.x;
+    // the eight classes of a column share its input: on one XCD (block b on XCD b mod 8)
+    const uint32_t col = blockIdx.x & 255u, c = blockIdx.x >> 8;
+    // w_{2^(t+4)}^(8j + c) = w_{2^(t+1)}^j * w_{2^(t+4)}^c: the standard stage
+    // table tw[0 .. 8192) (contiguous, L2-resident) times one factor per stage
+    for (uint32_t i = tid; i < P; i += TPB) {
+        const uint32_t t = 31u - __clz(i | 1u);
+        twc[i] = i ? mmul(tw[i], tw[(1u << (t + 3)) + c]) : 0u;
+    }
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a0 + (size_t)col * P);
+        uint4 v[4];
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++) v[r] = src[r * TPB + tid];
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++) {
+            const uint32_t x = 4u * (r * TPB + tid);
+            lds[ntt_laddr(x)] = v[r].x;
+            lds[ntt_laddr(x + 1)] = v[r].y;
+            lds[ntt_laddr(x + 2)] = v[r].z;
+            lds[ntt_laddr(x + 3)] = v[r].w;
+        }
+    }
+    __syncthreads();
+    uint32_t R[16];
+    // ---- phase 0: stages 0..3 on positions q = 16 tid + e, read bit-reversed
+#pragma unroll
+    for (int e = 0; e < 16; e++) R[e] = lds[ntt_laddr(__brev(16u * tid + (uint32_t)e) >> 19)];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            if (e & (1 << t)) continue;
+            const uint32_t u = R[e], v = mmul(R[e + (1 << t)], twc[(1u << t) + ((uint32_t)e & ((1u << t) - 1))]);
+            R[e] = add(u, v);
+            R[e + (1 << t)] = sub(u, v);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 16; e++) lds[ntt_laddr(16u * tid + e)] = R[e];
+    __syncthreads();
+    // ---- phase 1: stages 4..7, 16 positions at stride 16 --------------------
+    {
+        const uint32_t ql = tid & 15u, base = ql + (tid >> 4) * 256u;
+#pragma unroll
+        for (int m = 0; m < 16; m++) R[m] = lds[ntt_laddr(base + 16u * m)];
+#pragma unroll
+        for (int t = 4; t < 8; t++) {
+            const int tb = t - 4;
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                if (m & (1 << tb)) continue;
+                const uint32_t q = ql + 16u * (uint32_t)m;
+                const uint32_t u = R[m], v = mmul(R[m + (1 << tb)], twc[(1u << t) + (q & ((1u << t) - 1))]);
+                R[m] = add(u, v);
+                R[m + (1 << tb)] = sub(u, v);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++) lds[ntt_laddr(base + 16u * m)] = R[m];
+    }
+    __syncthreads();
+    // ---- phase 2: stages 8..11, 16 positions at stride 256 ------------------
+    {
+        const uint32_t ql = tid & 255u, base = ql + (tid >> 8) * 4096u;
+#pragma unroll
+        for (int m = 0; m < 16; m++) R[m] = lds[ntt_laddr(base + 256u * m)];
+#pragma unroll
+        for (int t = 8; t < 12; t++) {
+            const int tb = t - 8;
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                if (m & (1 << tb)) continue;
+                const uint32_t q = ql + 256u * (uint32_t)m;
+                const uint32_t u = R[m], v = mmul(R[m + (1 << tb)], twc[(1u << t) + (q & ((1u << t) - 1))]);
+                R[m] = add(u, v);
+                R[m + (1 << tb)] = sub(u, v);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++) lds[ntt_laddr(base + 256u * m)] = R[m];
+    }
+    __syncthreads();
+    // ---- stage 12 (pairs q, q + 4096) and the store: 8 consecutive q per lane
+    uint32_t* out = y + (size_t)c * ((size_t)1 << 21) + (size_t)col * P;
+    uint32_t lo[8], hi[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; i++) {
+        const uint32_t q = 8u * tid + i;
+        const uint32_t u = lds[ntt_laddr(q)], v = mmul(lds[ntt_laddr(q + 4096u)], twc[4096u + q]);
+        lo[i] = add(u, v);
+        hi[i] = sub(u, v);
+    }
+    uint4* o = reinterpret_cast<uint4*>(out + 8u * tid);
+    o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    o[1] = make_uint4(lo[4], lo[5], lo[6], lo[7]);
+    uint4* oh = reinterpret_cast<uint4*>(out + 4096u + 8u * tid);
+    oh[0] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    oh[1] = make_uint4(hi[4], hi[5], hi[6], hi[7]);
+}
+
 template <int NS>
 static void launch_first_wide(const uint32_t* src, size_t d, uint32_t* dst, uint32_t log_n, const NttPlan& p,
                               bool last, uint32_t z, hipStream_t s) {
@@ -638,6 +819,17 @@ void launch_ntt(const NttPlan& p, const uint32_t* src, size_t d, uint32_t* dst, 
     }
     uint32_t first = log_n % 8;
     if (first == 0) first = 8;
+#if NTT_LDE24
+    // 2^24 from <= 2^21 coefficients (blowup >= 8): gather + two passes (k_lde24_*)
+    if (log_n == 24 && p.scratch && !p.post_lo && d <= ((size_t)1 << 21) &&
+        ((((uintptr_t)src) | ((uintptr_t)dst) | ((uintptr_t)p.scratch)) & 15u) == 0) {
+        hipLaunchKernelGGL(k_lde24_gather, dim3(256), dim3(256), 0, s, src, d, dst, p.pre_lo, p.pre_hi);
+        hipLaunchKernelGGL(k_lde24_a, dim3(2048), dim3(512), 0, s, dst, p.scratch, p.tw);
+        hipLaunchKernelGGL((k_ntt_pass<4, 4, false, 512, 0, true, true>), dim3(2048), dim3(512), 0, s, p.scratch,
+                           (size_t)0, dst, 24u, 16u, p.tw, nullptr, nullptr, nullptr, nullptr);
+        return;
+    }
+#endif
 #if NTT_WIDE24
     // 2^24: two passes of 12 stages (k_ntt_first_wide<12> + k_ntt_later_wide12)
     if (log_n == 24 && ((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
