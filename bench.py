@@ -378,6 +378,23 @@ def main():
             ctx.commit(coeffs, log_n)
         pcie = {"ms_per_step": round(1000.0 * (time.perf_counter() - t0) / k, 4),
                 "what": f"fri_commit from a pageable host buffer of {d} u32 coefficients (H2D inside the call)"}
+        if mode == "single":
+            # the same host input through fri_commit_async, two commits in
+            # flight: the pinned copy and the upload (copy engine) of commit
+            # i+1 overlap commit i
+            outs = [fri_amd.CommitResult() for _ in range(k)]
+            for t in [ctx.commit_async(coeffs, log_n) for _ in range(2)]:    # warm-up: slot buffers and graphs
+                ctx.commit_wait(t)
+            t0 = time.perf_counter()
+            pend = []
+            for i in range(k):
+                pend.append(ctx.commit_async(coeffs, log_n))
+                if len(pend) == 2:
+                    ctx.commit_wait(pend.pop(0), outs[i - 1])
+            ctx.commit_wait(pend.pop(0), outs[k - 1])
+            pcie["pipelined_ms_per_step"] = round(1000.0 * (time.perf_counter() - t0) / k, 4)
+            pcie["pipelined_transcripts_ok"] = all(_same(o, res0) for o in outs)
+            pcie["pipelined_what"] = "fri_commit_async from the same host buffer, 2 commits in flight"
 
     # Decommitment (fri_commit.rs:137-179) on the commit
     # just made: one fri_decommit_query per query index gathers both values and

@@ -221,6 +221,12 @@ int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
 int fri_commit_device_async(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
                             uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                             const uint32_t* forced_betas, uint64_t* ticket);
+/* Same, from host coefficients: copied into a pinned buffer of the result
+ * slot before the call returns (the caller may reuse `coeffs` at once), then
+ * to the device as an asynchronous copy on the context stream. */
+int fri_commit_async(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n,
+                     uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                     const uint32_t* forced_betas, uint64_t* ticket);
 int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result* out);
 
 /* Which commit the read-backs below serve: `generation` grows with every

@@ -117,7 +117,11 @@ struct fri_ctx {
     uint64_t slot_ticket[FRI_MAX_INFLIGHT] = {};
     uint32_t slot_log_n[FRI_MAX_INFLIGHT] = {};
     bool slot_pending[FRI_MAX_INFLIGHT] = {};
-    bool slot_done[FRI_MAX_INFLIGHT] = {};  // the stream has passed the slot's event (settle)
+    uint32_t* h_in[FRI_MAX_INFLIGHT] = {};  // fri_commit_async: pinned copy of the slot's host coefficients,
+    uint32_t* d_slot_in[FRI_MAX_INFLIGHT] = {};   // its device copy (uploaded on h2d_stream while the
+    size_t h_in_cap[FRI_MAX_INFLIGHT] = {};       // previous commit runs) and the upload's event
+    hipEvent_t ev_in[FRI_MAX_INFLIGHT] = {};
+    hipStream_t h2d_stream = nullptr;
     uint64_t next_ticket = 1;
     bool async_unsettled = false;   // commits enqueued since the stream was last drained
     Plan plan;
@@ -330,7 +334,11 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     for (int i = 0; i < FRI_MAX_INFLIGHT; i++) {
         if (ctx->h_slot[i]) hipHostFree(ctx->h_slot[i]);
         if (ctx->ev_slot[i]) hipEventDestroy(ctx->ev_slot[i]);
+        if (ctx->h_in[i]) hipHostFree(ctx->h_in[i]);
+        dfree(ctx, ctx->d_slot_in[i]);
+        if (ctx->ev_in[i]) hipEventDestroy(ctx->ev_in[i]);
     }
+    if (ctx->h2d_stream) hipStreamDestroy(ctx->h2d_stream);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return FRI_OK;
@@ -1019,11 +1027,15 @@ extern "C" int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t 
     return run_commit(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
 }
 
-extern "C" int fri_commit_device_async(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
-                                       uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
-                                       const uint32_t* forced_betas, uint64_t* ticket) {
+// Pipelined commits: a free result slot, the commit enqueued with its state
+// in that slot, an event after its copy-out.  Host coefficients are first
+// copied into the slot's pinned buffer, so the caller may reuse its buffer at
+// once and the host-to-device copy is a true async copy on the stream.
+static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* d_coeffs, size_t d,
+                         uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                         const uint32_t* forced_betas, uint64_t* ticket) {
     if (!ctx || !ticket) return fail(ctx, FRI_EINVAL, "null argument");
-    if (d && !d_coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    if (d && !host_coeffs && !d_coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
     if (ctx->profiling) return fail(ctx, FRI_ESTATE, "profiling: time commits with fri_commit_device");
     int slot = -1;
     for (int i = 0; i < FRI_MAX_INFLIGHT && slot < 0; i++)
@@ -1034,6 +1046,31 @@ extern "C" int fri_commit_device_async(fri_ctx* ctx, const uint32_t* d_coeffs, s
         FRI_HIP(ctx, hipHostMalloc(&ctx->h_slot[slot], sizeof(DevState), hipHostMallocDefault));
         FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_slot[slot], hipEventDisableTiming));
     }
+    if (host_coeffs && d) {
+        // host input: pinned copy now, upload on h2d_stream (the copy engine,
+        // beside the commit still running), the commit stream waits for it and
+        // then moves it into the plan's input buffer (a device copy)
+        if (log_n >= 1 && log_n <= ctx->log_n_max && d > ((size_t)1 << log_n))
+            return fail(ctx, FRI_EDEGREE, "more coefficients than domain points (domain would be exhausted)");
+        if (d > ((size_t)1 << ctx->log_n_max)) return fail(ctx, FRI_EINVAL, "log_n out of range for context");
+        if (!ctx->h2d_stream) FRI_HIP(ctx, hipStreamCreateWithFlags(&ctx->h2d_stream, hipStreamNonBlocking));
+        if (!ctx->ev_in[slot]) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_in[slot], hipEventDisableTiming));
+        if (ctx->h_in_cap[slot] < d) {       // the slot is free: its last upload and commit have completed
+            if (ctx->h_in[slot]) hipHostFree(ctx->h_in[slot]);
+            dfree(ctx, ctx->d_slot_in[slot]);
+            ctx->h_in[slot] = ctx->d_slot_in[slot] = nullptr;
+            ctx->h_in_cap[slot] = 0;
+            FRI_HIP(ctx, hipHostMalloc(&ctx->h_in[slot], d * 4, hipHostMallocDefault));
+            if (dalloc(ctx, &ctx->d_slot_in[slot], d * 4) != hipSuccess) return fail(ctx, FRI_ENOMEM, "input slot");
+            ctx->h_in_cap[slot] = d;
+        }
+        memcpy(ctx->h_in[slot], host_coeffs, d * 4);
+        FRI_HIP(ctx, hipMemcpyAsync(ctx->d_slot_in[slot], ctx->h_in[slot], d * 4, hipMemcpyHostToDevice,
+                                    ctx->h2d_stream));
+        FRI_HIP(ctx, hipEventRecord(ctx->ev_in[slot], ctx->h2d_stream));
+        FRI_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_in[slot], 0));
+        d_coeffs = ctx->d_slot_in[slot];
+    }
     int rc = commit_enqueue(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, slot);
     if (rc) return rc;
     FRI_HIP(ctx, hipEventRecord(ctx->ev_slot[slot], ctx->stream));
@@ -1043,6 +1080,20 @@ extern "C" int fri_commit_device_async(fri_ctx* ctx, const uint32_t* d_coeffs, s
     ctx->async_unsettled = true;
     *ticket = ctx->slot_ticket[slot];
     return FRI_OK;
+}
+
+extern "C" int fri_commit_async(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t log_n, uint32_t offset,
+                                const fri_channel_state* chan_in, uint32_t flags, const uint32_t* forced_betas,
+                                uint64_t* ticket) {
+    if (d && !coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    return async_enqueue(ctx, coeffs, nullptr, d, log_n, offset, chan_in, flags, forced_betas, ticket);
+}
+
+extern "C" int fri_commit_device_async(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
+                                       uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                                       const uint32_t* forced_betas, uint64_t* ticket) {
+    if (d && !d_coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    return async_enqueue(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, ticket);
 }
 
 extern "C" int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result* out) {

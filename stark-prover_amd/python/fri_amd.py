@@ -102,6 +102,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_commit_device_async": (i32, [vp, vp, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
                                           ctypes.POINTER(ctypes.c_uint64)]),
         "fri_commit_wait": (i32, [vp, ctypes.c_uint64, ctypes.POINTER(CommitResult)]),
+        "fri_commit_async": (i32, [vp, pu32, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
+                                   ctypes.POINTER(ctypes.c_uint64)]),
         "fri_ctx_input_buffer": (i32, [vp, sz, ctypes.POINTER(vp)]),
         "fri_commit_info": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "fri_layer_copy": (i32, [vp, u32, pu32, sz]),
@@ -272,6 +274,20 @@ class Context:
         t = ctypes.c_uint64()
         self._check(self.lib.fri_commit_device_async(self.h, d_coeffs, d, log_n, offset, ctypes.byref(ch), 0, None,
                                                      ctypes.byref(t)))
+        return t.value
+
+    def commit_async(self, coeffs, log_n: int, offset: int = GENERATOR,
+                     channel_state: Optional[bytes] = None) -> int:
+        """Enqueue a commit of host coefficients and return its ticket
+        (fri_commit_async: the coefficients are copied before it returns)."""
+        c = _u32(coeffs)
+        ch = ChannelState()
+        if channel_state:
+            ctypes.memmove(ch.digest, channel_state, 32)
+            ch.has_state = 1
+        t = ctypes.c_uint64()
+        self._check(self.lib.fri_commit_async(self.h, _ptr(c), c.size, log_n, offset, ctypes.byref(ch), 0, None,
+                                              ctypes.byref(t)))
         return t.value
 
     def commit_wait(self, ticket: int, out: Optional[CommitResult] = None) -> CommitResult:

@@ -202,3 +202,32 @@ def test_pipelined_then_sharded_on_one_context(oracle, oracle_commit, torch):
         assert _transcript(cx.commit_wait(t2)) == oracle_commit(log_n, 961)
     finally:
         cx.close()
+
+
+def test_pipelined_host_input(pctx, oracle, oracle_commit):
+    """fri_commit_async: host coefficients are copied before the call
+    returns, so one host buffer can be refilled for the next commit while the
+    earlier ones are still pending; every transcript equals the oracle's."""
+    import fri_amd
+    d = (1 << LOG_N) >> 3
+    buf = np.empty(d, dtype=np.uint32)
+    seeds = [971, 972, 973, 974]
+    tickets = []
+    for s in seeds:
+        buf[:] = oracle.splitmix64_np(s, d).astype(np.uint32)
+        tickets.append(pctx.commit_async(buf, LOG_N))
+    buf[:] = 0                                               # the pending commits do not see this
+    for t, s in zip(tickets, seeds):
+        assert _transcript(pctx.commit_wait(t)) == oracle_commit(LOG_N, s)
+    with pytest.raises(fri_amd.FriError) as e:
+        pctx.commit_async(np.zeros((1 << LOG_N) + 1, dtype=np.uint32), LOG_N)    # d > n
+    assert e.value.code == fri_amd.FRI_EDEGREE
+    bad = oracle.splitmix64_np(975, d).astype(np.uint32)
+    bad[7] = P_BAD
+    t = pctx.commit_async(bad, LOG_N)
+    with pytest.raises(fri_amd.FriError) as e:
+        pctx.commit_wait(t)
+    assert e.value.code == fri_amd.FRI_EINVAL
+
+
+P_BAD = 3221225473                                           # p itself: not canonical
