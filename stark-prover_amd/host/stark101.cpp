@@ -319,14 +319,53 @@ FRIProof fri_commit_coset(const Poly& poly, uint32_t log_n, FE offset, FriChanne
     return FRIProof::mirror(res, log_n, gpu, channel);
 }
 
+std::vector<FRIProof> fri_commit_pipelined(const std::vector<Poly>& polys, uint32_t log_n, FE offset,
+                                           std::vector<FriChannel>& channels, const std::shared_ptr<Gpu>& gpu) {
+    if (!gpu) throw Panic("fri_commit: no Gpu");
+    if (channels.size() != polys.size()) throw Panic("fri_commit_pipelined: one channel per polynomial");
+    if (log_n > gpu->log_n_max()) throw Panic("fri_commit: codeword 2^" + std::to_string(log_n) + " exceeds the context");
+    struct Pending { size_t i; uint64_t ticket, gen; };
+    std::vector<FRIProof> out(polys.size());
+    std::vector<Pending> pend;
+    auto collect = [&](const Pending& p) {
+        fri_commit_result res{};
+        gpu->check(fri_commit_wait(gpu->ctx(), p.ticket, &res), "fri_commit_wait");
+        out[p.i] = FRIProof::mirror(res, log_n, gpu, channels[p.i], p.gen);
+    };
+    for (size_t i = 0; i < polys.size(); i++) {
+        if (pend.size() == 2) {
+            collect(pend.front());
+            pend.erase(pend.begin());
+        }
+        std::vector<uint32_t> coeffs = to_u32(polys[i].coefficients);
+        fri_channel_state cin{};
+        const fri_channel_state* pin = nullptr;
+        if (!channels[i].state.empty()) {
+            auto st = sha::from_hex(channels[i].state);
+            if (st.size() != 32) throw Panic("Channel state is not a SHA-256 digest");
+            std::memcpy(cin.digest, st.data(), 32);
+            cin.has_state = 1;
+            pin = &cin;
+        }
+        uint64_t ticket = 0;
+        const uint64_t gen = gpu->bump();          // this commit's layers replace the previous ones
+        gpu->check(fri_commit_async(gpu->ctx(), coeffs.data(), coeffs.size(), log_n,
+                                    static_cast<uint32_t>(offset.value()), pin, 0, nullptr, &ticket),
+                   "fri_commit_async");
+        pend.push_back({i, ticket, gen});
+    }
+    for (const Pending& p : pend) collect(p);
+    return out;
+}
+
 FRIProof FRIProof::mirror(const fri_commit_result& res, uint32_t log_n, const std::shared_ptr<Gpu>& gpu,
-                          FriChannel& channel) {
+                          FriChannel& channel, uint64_t gen) {
     // The channel messages the reference's loop produced (fri_commit.rs:84-114):
     // root_hex bytes per layer, beta (8 B BE, proof only) per round, final value.
     FRIProof proof;
     proof.log_n = log_n;
     proof.gpu_ = gpu;
-    proof.gen_ = gpu->generation();
+    proof.gen_ = gen ? gen : gpu->generation();
     for (uint32_t k = 0; k < res.n_layers; k++) {
         const std::string hex = sha::hex(res.roots[k], 32);
         std::vector<uint8_t> msg(hex.begin(), hex.end());

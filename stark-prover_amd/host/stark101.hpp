@@ -290,6 +290,8 @@ class MerkleTree {
   private:
     friend class FRIProof;
     friend FRIProof fri_commit_coset(const Poly&, uint32_t, FE, FriChannel&, const std::shared_ptr<Gpu>&);
+    friend std::vector<FRIProof> fri_commit_pipelined(const std::vector<Poly>&, uint32_t, FE, std::vector<FriChannel>&,
+                                                      const std::shared_ptr<Gpu>&);
     MerkleTree() = default;
     std::string root_hex_;
     std::shared_ptr<Gpu> gpu_;
@@ -313,13 +315,16 @@ class FRIProof {
 
   private:
     friend FRIProof fri_commit_coset(const Poly&, uint32_t, FE, FriChannel&, const std::shared_ptr<Gpu>&);
+    friend std::vector<FRIProof> fri_commit_pipelined(const std::vector<Poly>&, uint32_t, FE, std::vector<FriChannel>&,
+                                                      const std::shared_ptr<Gpu>&);
     friend void decommit_fri_layers(size_t, const FRIProof&, FriChannel&);
     friend StarkProof prove_fibsq(FE, uint32_t, uint32_t, size_t, FriChannel&, FE, std::shared_ptr<Gpu>);
     // The proof of a device commit: appends the messages the device sent
     // (root hex per layer, beta per round, final value) to `channel` and
     // takes over its state (fri_commit.rs:84-114).
+    // gen: the Gpu generation of that commit (default: the current one).
     static FRIProof mirror(const fri_commit_result& res, uint32_t log_n, const std::shared_ptr<Gpu>& gpu,
-                           FriChannel& channel);
+                           FriChannel& channel, uint64_t gen = 0);
     std::shared_ptr<Gpu> gpu_;
     uint64_t gen_ = 0;
     void require_resident() const;
@@ -335,6 +340,14 @@ FRIProof fri_commit(const Poly& poly, const Coset& coset, FriChannel& channel);
 // Explicit context (log_n <= gpu->log_n_max()).
 FRIProof fri_commit_coset(const Poly& poly, uint32_t log_n, FE offset, FriChannel& channel,
                           const std::shared_ptr<Gpu>& gpu);
+
+// fri_commit (fri_commit.rs:72-122) of many polynomials in a row, each with
+// its own channel, pipelined on one Gpu (fri_commit_async / fri_commit_wait,
+// two in flight: the next upload overlaps the running commit).  Proof i equals
+// fri_commit_coset(polys[i], ..., channels[i]); only the last proof's layers
+// and trees stay resident (the earlier ones report resident() == false).
+std::vector<FRIProof> fri_commit_pipelined(const std::vector<Poly>& polys, uint32_t log_n, FE offset,
+                                           std::vector<FriChannel>& channels, const std::shared_ptr<Gpu>& gpu);
 
 // fri_commit.rs:137-179 over the device-resident layers and trees.
 void decommit_fri_layers(size_t index, const FRIProof& proof, FriChannel& channel);

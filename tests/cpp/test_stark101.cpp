@@ -12,6 +12,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "stark101.hpp"
@@ -363,6 +364,46 @@ TEST(gpu, fri_commit_and_decommit_match_golden) {
     }
     ASSERT_TRUE(checked >= 30);
 }
+// fri_commit_pipelined: the golden cases grouped by (log_n, offset), each
+// group committed back to back on one Gpu (two in flight); every proof and
+// channel equals the golden transcript, and only the last proof of a group
+// keeps its layers resident (its decommitment matches the golden one).
+TEST(gpu, fri_commit_pipelined_matches_golden) {
+    std::map<std::pair<uint32_t, uint64_t>, std::vector<const GoldenCase*>> groups;
+    for (const auto& c : GOLDEN)
+        if (!c.forced) groups[{c.log_n, c.offset}].push_back(&c);
+    int checked = 0;
+    for (auto& g : groups) {
+        const auto& cases = g.second;
+        if (cases.size() < 2) continue;
+        auto gpu = std::make_shared<Gpu>(0, g.first.first < 10 ? 10 : g.first.first);
+        std::vector<Poly> polys;
+        std::vector<FriChannel> chans(cases.size());
+        for (size_t i = 0; i < cases.size(); i++) {
+            polys.push_back(poly_of(*cases[i]));
+            chans[i].state = cases[i]->channel_in;
+        }
+        std::vector<FRIProof> proofs = fri_commit_pipelined(polys, g.first.first, FE(g.first.second), chans, gpu);
+        for (size_t i = 0; i < cases.size(); i++) {
+            const GoldenCase& c = *cases[i];
+            ASSERT_EQ(proofs[i].n_layers(), c.roots.size());
+            for (size_t k = 0; k < c.roots.size(); k++) ASSERT_EQ(proofs[i].fri_merkles[k].root(), std::string(c.roots[k]));
+            for (size_t k = 0; k < c.betas.size(); k++) ASSERT_EQ(proofs[i].betas[k].value(), c.betas[k]);
+            ASSERT_EQ(chans[i].state, std::string(c.channel_out));
+            ASSERT_EQ(chans[i].proof_size(), c.proof_size);
+            ASSERT_TRUE(proofs[i].resident() == (i + 1 == cases.size()));
+            checked++;
+        }
+        const GoldenCase& last = *cases.back();
+        FriChannel& ch = chans.back();
+        const size_t n_commit = ch.proof.size();
+        decommit_fri(3, (size_t{1} << last.log_n) - 1, proofs.back(), ch);
+        ASSERT_EQ(ch.state, std::string(last.dq3_state));
+        ASSERT_EQ(transcript_sha(ch.proof, n_commit), std::string(last.dq3_sha));
+    }
+    ASSERT_TRUE(checked >= 4);
+}
+
 // The FRIProof's device-resident MerkleTree (get_authentication_path ->
 // fri_auth_path, one gather launch) and the query gather (fri_decommit_query)
 // serve the same rs_merkle paths, and each path hashes up to its layer root.

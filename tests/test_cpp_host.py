@@ -71,4 +71,5 @@ def test_host_library_exports_reference_api():
 def test_cpp_host_mirror_gpu():
     out = _run("gpu")
     assert "ok   gpu::fri_commit_and_decommit_match_golden" in out
+    assert "ok   gpu::fri_commit_pipelined_matches_golden" in out
     assert "ok   gpu::prove_fibsq_matches_golden" in out
