@@ -896,6 +896,34 @@ def fri_commit(coeffs: Sequence[int], log_n: int, channel: Channel, offset: int 
     return _mirror_commit(res, ctx, log_n, channel)
 
 
+def fri_commit_pipelined(polys: Sequence[Sequence[int]], log_n: int, channels: Sequence[Channel],
+                         offset: int = GENERATOR, ctx: Optional[Context] = None, depth: int = 2) -> List[FRIProof]:
+    """fri_commit (fri_commit.rs:72-122) of many polynomials in a row, each
+    with its own channel, ``depth`` commits in flight on one context
+    (fri_commit_async / fri_commit_wait): proof i equals fri_commit of
+    polys[i] into channels[i]; only the last proof's layers stay resident."""
+    if len(polys) != len(channels):
+        raise FriError(FRI_EINVAL, "one channel per polynomial")
+    if not 1 <= depth <= MAX_INFLIGHT:
+        raise FriError(FRI_EINVAL, "depth must be 1..MAX_INFLIGHT")
+    ctx = ctx or _default_ctx(log_n)
+    g0 = ctx.commit_info()[0]           # every enqueued commit bumps the generation by one
+    out: List[Optional[FRIProof]] = [None] * len(polys)
+    pend = []
+
+    def collect(i, ticket):
+        out[i] = _mirror_commit(ctx.commit_wait(ticket), ctx, log_n, channels[i], generation=g0 + i + 1)
+
+    for i, (c, ch) in enumerate(zip(polys, channels)):
+        if len(pend) == depth:
+            collect(*pend.pop(0))
+        st = bytes.fromhex(ch.state) if ch.state else None
+        pend.append((i, ctx.commit_async(c, log_n, offset, channel_state=st)))
+    for p in pend:
+        collect(*p)
+    return out
+
+
 def fri_commit_sharded(coeffs: Sequence[int], log_n: int, channel: Channel, ctx: Context,
                        offset: int = GENERATOR) -> FRIProof:
     """fri_commit (fri_commit.rs:72-122) over the ranks attached to ``ctx``
@@ -909,7 +937,8 @@ def fri_commit_sharded(coeffs: Sequence[int], log_n: int, channel: Channel, ctx:
     return proof
 
 
-def _mirror_commit(res: CommitResult, ctx: Context, log_n: int, channel: Channel) -> FRIProof:
+def _mirror_commit(res: CommitResult, ctx: Context, log_n: int, channel: Channel,
+                   generation: Optional[int] = None) -> FRIProof:
     """Append the messages the device commit sent (root hex per layer, beta
     per round, final value) to ``channel`` and take over its state."""
     roots = [bytes(res.roots[k]) for k in range(res.n_layers)]
@@ -923,4 +952,5 @@ def _mirror_commit(res: CommitResult, ctx: Context, log_n: int, channel: Channel
     channel.proof.append(fv)
     channel.compressed_proof.append(fv)
     channel.state = bytes(res.channel_out.digest).hex() if res.channel_out.has_state else ""
-    return FRIProof(ctx, log_n, roots, betas, int(res.final_value), int(res.final_degree), ctx.commit_info()[0])
+    gen = ctx.commit_info()[0] if generation is None else generation
+    return FRIProof(ctx, log_n, roots, betas, int(res.final_value), int(res.final_degree), gen)

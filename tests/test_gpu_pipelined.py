@@ -231,3 +231,42 @@ def test_pipelined_host_input(pctx, oracle, oracle_commit):
 
 
 P_BAD = 3221225473                                           # p itself: not canonical
+
+
+def test_python_mirror_pipelined_matches_golden(golden, oracle):
+    """fri_amd.fri_commit_pipelined over the golden cases grouped by
+    (log_n, offset): every proof and channel equals the golden transcript;
+    only the last proof of a group serves read-backs, and its decommitment
+    (decommit_fri, fri_commit.rs:168-179) equals the golden one."""
+    import fri_amd
+    groups = {}
+    for c in golden["cases"]:
+        if not c["forced_betas"]:
+            groups.setdefault((c["log_n"], c["offset"]), []).append(c)
+    checked = 0
+    for (log_n, offset), cases in groups.items():
+        if len(cases) < 2:
+            continue
+        cx = fri_amd.Context(0, max(log_n, 10))
+        try:
+            chans = []
+            for c in cases:
+                ch = fri_amd.Channel()
+                ch.state = c["channel_in"]
+                chans.append(ch)
+            proofs = fri_amd.fri_commit_pipelined([c["coeffs"] for c in cases], log_n, chans, offset, ctx=cx)
+            for i, (c, pr, ch) in enumerate(zip(cases, proofs, chans)):
+                assert [r.hex() for r in pr.roots] == c["roots"]
+                assert pr.betas == c["betas"]
+                assert ch.state == c["channel_out"] and ch.proof_size() == c["proof_size"]
+                if i + 1 < len(cases):
+                    with pytest.raises(fri_amd.FriError):
+                        pr.layer(0)                                  # replaced by a later commit
+                checked += 1
+            last, ch = cases[-1], chans[-1]
+            n0 = len(ch.proof)
+            fri_amd.decommit_fri(3, (1 << log_n) - 1, proofs[-1], ch)
+            assert ch.state == last["decommit_q3"]["state"]
+        finally:
+            cx.close()
+    assert checked >= 4
