@@ -369,6 +369,21 @@ def main():
              "frac_of_hbm_peak": round((b_field + b_tree) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
              "sha256_compressions": sha_compressions(log_n, d)}
 
+    # (run before any stage that creates streams of its own: each context's
+    # stream should get a hardware queue of its own, GPU_MAX_HW_QUEUES = 4)
+    # Serving throughput: C independent commits in flight on one GPU (one
+    # context + stream per host thread, the documented multi-context use).
+    # The tree tops of one commit (one workgroup on the serial Fiat-Shamir
+    # chain) overlap the leaf hashing of the others.  Beside `value`, never it.
+    concurrent = None
+    pipelined = None
+    if world == 1 and mode == "single" and log_n >= 20:
+        pipelined = _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps=args.steps)
+    if world == 1 and mode == "single" and log_n >= 20 and not args.no_extras:
+        single = _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K=4, steps=max(12, args.steps))
+        concurrent = _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C=3, steps=max(5, args.steps // 2))
+        concurrent["single_thread_async"] = single
+
     # PCIe-inclusive rate (host coefficients in, result out): never `value`
     pcie = None
     if world == 1 and not args.no_extras:
@@ -417,17 +432,6 @@ def main():
         trace_stage = {"ms_per_call": round(1000.0 * (time.perf_counter() - t0) / k, 4),
                        "what": "fri_trace_commit: 2^16 trace -> iNTT -> LDE on 5*<w_2^19> -> SHA-256 Merkle "
                                "(host trace in, root + coefficients + LDE read back)"}
-
-    # Serving throughput: C independent commits in flight on one GPU (one
-    # context + stream per host thread, the documented multi-context use).
-    # The tree tops of one commit (one workgroup on the serial Fiat-Shamir
-    # chain) overlap the leaf hashing of the others.  Beside `value`, never it.
-    concurrent = None
-    pipelined = None
-    if world == 1 and mode == "single" and log_n >= 20:
-        pipelined = _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps=args.steps)
-    if world == 1 and mode == "single" and log_n >= 20 and not args.no_extras:
-        concurrent = _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C=3, steps=max(5, args.steps // 2))
 
     # Whole prover slice, BASELINE configs[3]: STARK-101 FibonacciSq trace of
     # 2^16 rows -> LDE 2^19 + Merkle -> alphas -> composition polynomial ->
@@ -602,6 +606,44 @@ def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps, depth=2):
             "transcripts_ok": all(_same(r, res0) for r in out),
             "what": f"{steps} commits of 2^{log_n} on one fri_ctx, up to {depth} enqueued "
                     "(fri_commit_device_async / fri_commit_wait): no host turnaround between commits"}
+
+
+def _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K, steps, depth=2):
+    """K contexts (one stream each) driven from ONE host thread: commits of
+    resident coefficients dealt round-robin with fri_commit_device_async, up
+    to `depth` in flight per context, collected with fri_commit_wait."""
+    ctxs, ptrs = [ctx], [dptr]
+    for _ in range(1, K):
+        cx = fri_amd.Context(ctx_device(ctx), log_n)
+        cx.commit(_coeffs(42, d, fri_amd.P), log_n)
+        p = ctypes.c_void_p()
+        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p)))
+        ctxs.append(cx)
+        ptrs.append(p)
+
+    def run(n, outs):
+        pend = []
+        for i in range(n):
+            j = i % K
+            if len(pend) == depth * K:
+                jj, t, k = pend.pop(0)
+                ctxs[jj].commit_wait(t, outs[k])
+            pend.append((j, ctxs[j].commit_device_async(ptrs[j], d, log_n), i))
+        for jj, t, k in pend:
+            ctxs[jj].commit_wait(t, outs[k])
+
+    run(depth * K, [fri_amd.CommitResult() for _ in range(depth * K)])       # warm-up: slot graphs
+    outs = [fri_amd.CommitResult() for _ in range(steps)]
+    t0 = time.perf_counter()
+    run(steps, outs)
+    wall = time.perf_counter() - t0
+    ok = all(_same(r, res0) for r in outs)
+    for cx in ctxs[1:]:
+        cx.close()
+    return {"contexts": K, "in_flight_per_context": depth, "ms_per_commit": round(1000.0 * wall / steps, 4),
+            "value": round(steps * (1 << log_n) / wall, 1), "unit": "field-elems/s", "transcripts_ok": ok,
+            "what": f"one host thread, {K} fri_ctx (one stream each), {steps} commits of 2^{log_n} dealt round-robin "
+                    "with fri_commit_device_async / fri_commit_wait"}
 
 
 def ctx_device(ctx):

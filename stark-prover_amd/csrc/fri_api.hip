@@ -121,7 +121,7 @@ struct fri_ctx {
     uint32_t* d_slot_in[FRI_MAX_INFLIGHT] = {};   // its device copy (uploaded on h2d_stream while the
     size_t h_in_cap[FRI_MAX_INFLIGHT] = {};       // previous commit runs) and the upload's event
     hipEvent_t ev_in[FRI_MAX_INFLIGHT] = {};
-    hipStream_t h2d_stream = nullptr;
+    hipStream_t h2d_stream = nullptr;   // the device's shared upload stream (upload_stream())
     uint64_t next_ticket = 1;
     bool async_unsettled = false;   // commits enqueued since the stream was last drained
     Plan plan;
@@ -338,7 +338,6 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
         dfree(ctx, ctx->d_slot_in[i]);
         if (ctx->ev_in[i]) hipEventDestroy(ctx->ev_in[i]);
     }
-    if (ctx->h2d_stream) hipStreamDestroy(ctx->h2d_stream);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return FRI_OK;
@@ -1027,6 +1026,23 @@ extern "C" int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t 
     return run_commit(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
 }
 
+// One upload stream per device, shared by every context of the process: a
+// context per host thread or several contexts driven from one thread (one
+// commit stream each) then add one stream in all, not one each, and stay
+// within the device's hardware queues (GPU_MAX_HW_QUEUES, 4 by default).
+// Created on first use and kept for the life of the process.
+static hipError_t upload_stream(int device, hipStream_t* out) {
+    static std::mutex m;
+    static std::map<int, hipStream_t> streams;
+    std::lock_guard<std::mutex> g(m);
+    auto it = streams.find(device);
+    if (it != streams.end()) { *out = it->second; return hipSuccess; }
+    hipStream_t st = nullptr;
+    const hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) streams[device] = *out = st;
+    return e;
+}
+
 // Pipelined commits: a free result slot, the commit enqueued with its state
 // in that slot, an event after its copy-out.  Host coefficients are first
 // copied into the slot's pinned buffer, so the caller may reuse its buffer at
@@ -1053,7 +1069,7 @@ static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32
         if (log_n >= 1 && log_n <= ctx->log_n_max && d > ((size_t)1 << log_n))
             return fail(ctx, FRI_EDEGREE, "more coefficients than domain points (domain would be exhausted)");
         if (d > ((size_t)1 << ctx->log_n_max)) return fail(ctx, FRI_EINVAL, "log_n out of range for context");
-        if (!ctx->h2d_stream) FRI_HIP(ctx, hipStreamCreateWithFlags(&ctx->h2d_stream, hipStreamNonBlocking));
+        if (!ctx->h2d_stream) FRI_HIP(ctx, upload_stream(ctx->device, &ctx->h2d_stream));
         if (!ctx->ev_in[slot]) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_in[slot], hipEventDisableTiming));
         if (ctx->h_in_cap[slot] < d) {       // the slot is free: its last upload and commit have completed
             if (ctx->h_in[slot]) hipHostFree(ctx->h_in[slot]);

@@ -897,28 +897,34 @@ def fri_commit(coeffs: Sequence[int], log_n: int, channel: Channel, offset: int 
 
 
 def fri_commit_pipelined(polys: Sequence[Sequence[int]], log_n: int, channels: Sequence[Channel],
-                         offset: int = GENERATOR, ctx: Optional[Context] = None, depth: int = 2) -> List[FRIProof]:
+                         offset: int = GENERATOR, ctx=None, depth: int = 2) -> List[FRIProof]:
     """fri_commit (fri_commit.rs:72-122) of many polynomials in a row, each
-    with its own channel, ``depth`` commits in flight on one context
-    (fri_commit_async / fri_commit_wait): proof i equals fri_commit of
-    polys[i] into channels[i]; only the last proof's layers stay resident."""
+    with its own channel, pipelined from this one host thread
+    (fri_commit_async / fri_commit_wait, ``depth`` commits in flight per
+    context).  ``ctx`` is one Context or a list of them: with several, the
+    commits are dealt round-robin and run concurrently, one stream each.
+    Proof i equals fri_commit of polys[i] into channels[i]; on each context
+    only its last proof's layers stay resident."""
     if len(polys) != len(channels):
         raise FriError(FRI_EINVAL, "one channel per polynomial")
     if not 1 <= depth <= MAX_INFLIGHT:
         raise FriError(FRI_EINVAL, "depth must be 1..MAX_INFLIGHT")
-    ctx = ctx or _default_ctx(log_n)
-    g0 = ctx.commit_info()[0]           # every enqueued commit bumps the generation by one
+    ctxs = list(ctx) if isinstance(ctx, (list, tuple)) else [ctx or _default_ctx(log_n)]
+    gen = [c.commit_info()[0] for c in ctxs]     # every enqueued commit bumps its context's generation by one
     out: List[Optional[FRIProof]] = [None] * len(polys)
     pend = []
 
-    def collect(i, ticket):
-        out[i] = _mirror_commit(ctx.commit_wait(ticket), ctx, log_n, channels[i], generation=g0 + i + 1)
+    def collect(i, j, ticket, g):
+        out[i] = _mirror_commit(ctxs[j].commit_wait(ticket), ctxs[j], log_n, channels[i], generation=g)
 
     for i, (c, ch) in enumerate(zip(polys, channels)):
-        if len(pend) == depth:
+        j = i % len(ctxs)
+        if len(pend) == depth * len(ctxs):
             collect(*pend.pop(0))
         st = bytes.fromhex(ch.state) if ch.state else None
-        pend.append((i, ctx.commit_async(c, log_n, offset, channel_state=st)))
+        t = ctxs[j].commit_async(c, log_n, offset, channel_state=st)
+        gen[j] += 1
+        pend.append((i, j, t, gen[j]))
     for p in pend:
         collect(*p)
     return out

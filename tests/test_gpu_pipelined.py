@@ -270,3 +270,32 @@ def test_python_mirror_pipelined_matches_golden(golden, oracle):
         finally:
             cx.close()
     assert checked >= 4
+
+
+def test_python_mirror_pipelined_over_contexts(oracle, oracle_commit):
+    """Several contexts driven from one host thread (commits dealt
+    round-robin, concurrent on their streams): every transcript equals the
+    oracle's, and on each context only its last proof is resident."""
+    import fri_amd
+    log_n = 16
+    d = (1 << log_n) >> 3
+    seeds = list(range(981, 988))
+    ctxs = [fri_amd.Context(0, log_n) for _ in range(3)]
+    try:
+        chans = [fri_amd.Channel() for _ in seeds]
+        proofs = fri_amd.fri_commit_pipelined([oracle.splitmix64_np(s, d).astype(np.uint32) for s in seeds],
+                                              log_n, chans, ctx=ctxs)
+        for s, pr, ch in zip(seeds, proofs, chans):
+            want = oracle_commit(log_n, s)
+            assert [r.hex() for r in pr.roots] == want["roots"] and pr.betas == want["betas"]
+            assert ch.state == want["state"]
+        for i, pr in enumerate(proofs):
+            last_on_ctx = i + len(ctxs) >= len(proofs)
+            if last_on_ctx:
+                assert pr.layer(1).size == 1 << (log_n - 1)
+            else:
+                with pytest.raises(fri_amd.FriError):
+                    pr.layer(0)
+    finally:
+        for c in ctxs:
+            c.close()
