@@ -309,6 +309,9 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     if (!ctx) return FRI_EINVAL;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    // an upload whose commit was never enqueued (it failed) may still read
+    // this context's pinned input buffers on the shared upload stream
+    if (ctx->h2d_stream) hipStreamSynchronize(ctx->h2d_stream);
     plan_free(ctx);
     for (auto e : ctx->event_pool) hipEventDestroy(e);
     fri_dist_detach(ctx);
