@@ -304,8 +304,12 @@ int fri_dist_selftest(fri_ctx* ctx, size_t words_per_peer);
  * channel state and gets the same result.  world == 1 is fri_commit.
  * Each rank's plan is shard-sized: it allocates only its block of every
  * sharded layer and tree and the x^-1 slices its folds read (plus the full
- * coefficient vector and the < 2^20 local tail), so a context created with
- * log_n_max = log_n - log2(world) suffices (2^28 over 8 ranks: ~6 GiB each).
+ * coefficient vector, which the coset LDE reads, and the < 2^20 local tail),
+ * so a context created with log_n_max = log_n - log2(world) suffices (2^28
+ * over 8 ranks: ~6 GiB each).  The coefficient fold that tracks the degree
+ * (next_fri_polynomial, fri_commit.rs:32-50,89) is sharded too: rank r folds
+ * coefficients [r*S_k, (r+1)*S_k) of poly_k, and the maxima that give the
+ * degree travel with the block roots in the per-layer all-gather.
  * Afterwards fri_layer_copy / fri_tree_level_copy / fri_auth_path serve the
  * layers finished on every rank (the < 2^20 tail); the sharded layers return
  * FRI_ESTATE (each rank holds only its block). */
@@ -365,6 +369,39 @@ int fri_debug_inject_stall(fri_ctx* ctx, int enable);
  * on data of the right shape with no host round trip, but the transcript is
  * not the real one (tools/shard_projection.py). */
 int fri_debug_attach_loopback(fri_ctx* ctx, int rank, int world);
+/* The degree schedule of the loopback rehearsal: deg[k] for every layer k of
+ * a 1-GPU commit of the same polynomial (fri_commit_degrees).  The sharded
+ * coefficient fold gives each rank only its slice of the degree maxima, and
+ * the loopback all-gather returns this rank's own slice G times, so without
+ * the recorded schedule the rehearsal would run fewer rounds than the real
+ * commit.  deg = NULL or n = 0 clears it. */
+int fri_debug_loopback_degrees(fri_ctx* ctx, const int32_t* deg, uint32_t n);
+
+/* Degree of poly_k for every layer k of the resident commit (the
+ * reference's Polynomial degree field, src/polynomial/ops.rs:47-60, as the
+ * loop of fri_commit.rs:89 sees it): out[k], k < *n_out = n_layers. */
+int fri_commit_degrees(fri_ctx* ctx, int32_t* out, size_t cap, uint32_t* n_out);
+
+/* Transport schedule of the last sharded call on the context
+ * (fri_commit_sharded*, fri_decommit_query_sharded, fri_dist_selftest): one
+ * entry per collective in issue order.  chan 0 = the main communicator on the
+ * context stream, 1 = the exchange communicator on the exchange stream (the
+ * logical channel; the host transport runs both on the context stream).  An
+ * RCCL run is deadlock-free when, per channel, every rank issues the same
+ * sequence of (op, bytes) and each SENDRECV at position i with peer q is
+ * matched by q's SENDRECV at position i with peer = this rank;
+ * the multi-rank tests check exactly that on every rank's log. */
+#define FRI_OP_ALLGATHER 1
+#define FRI_OP_ALLTOALL  2
+#define FRI_OP_SENDRECV  3
+typedef struct {
+    uint32_t chan;      /* 0: main, 1: exchange                                   */
+    uint32_t op;        /* FRI_OP_*                                                */
+    int32_t  peer;      /* SENDRECV partner; -1 for collectives                    */
+    uint32_t reserved;
+    uint64_t bytes;     /* ALLGATHER: per rank; ALLTOALL: per peer; SENDRECV: each way */
+} fri_transport_op;
+int fri_debug_transport_log(fri_ctx* ctx, fri_transport_op* out, size_t cap, size_t* count);
 
 #ifdef __cplusplus
 }

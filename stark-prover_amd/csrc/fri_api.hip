@@ -41,6 +41,11 @@ struct Plan {
     bool sharded = false;
     uint32_t G = 1, rank = 0;
     int k_sw = -1;
+    // Sharded coefficient fold: rank r holds coefficients [r*S_k, (r+1)*S_k)
+    // of poly_k, S_k = 2^(cs0 - k), for k = 1..k_sw (coefA/B hold chunks);
+    // coefF receives poly_{k_sw} whole at the switch to the local tail.
+    uint32_t cs0 = 0;
+    uint32_t* coefF = nullptr;  size_t coefF_cap = 0;
     uint32_t* d_in = nullptr;   size_t in_cap = 0;
     uint32_t* coefA = nullptr;
     uint32_t* coefB = nullptr;  size_t coef_cap = 0;
@@ -73,6 +78,7 @@ struct Transport {
     uint8_t* hs = nullptr;      // pinned staging
     uint8_t* hr = nullptr;
     size_t hcap = 0;
+    std::vector<fri_transport_op> log;   // schedule of the last sharded call (fri_debug_transport_log)
 };
 
 // Scratch of the sharded commit (sized on first use).
@@ -88,6 +94,11 @@ struct DistBuf {
     size_t gcap = 0;            // words in gath
     uint32_t* gath = nullptr;   // all-gathered layer at the switch to local
     uint32_t* dq = nullptr;     // sharded decommitment: this rank's openings + all ranks' (G + 1 slots)
+    uint32_t* rec = nullptr;    // per-layer record: this rank's (REC_WORDS) then all ranks' (64 * REC_WORDS)
+    int32_t* mx = nullptr;      // the G maxima triples of the current layer (k_tree_top's producers)
+    uint32_t* c0 = nullptr;     // poly_k coefficient 0 (the final value when deg_k = 0)
+    int32_t* sched = nullptr;   // loopback rehearsal: recorded degree per layer (fri_debug_loopback_degrees),
+    std::vector<int32_t> sched_h;   // uploaded by the next sharded commit
 };
 
 // One timed launch group: events recorded around it on the context stream.
@@ -300,7 +311,7 @@ static void plan_free(fri_ctx* ctx) {
     }
     if (p.tail_exec) hipGraphExecDestroy(p.tail_exec);
     if (p.tail_graph) hipGraphDestroy(p.tail_graph);
-    dfree(ctx, p.d_in); dfree(ctx, p.coefA); dfree(ctx, p.coefB); dfree(ctx, p.layers);
+    dfree(ctx, p.d_in); dfree(ctx, p.coefA); dfree(ctx, p.coefB); dfree(ctx, p.coefF); dfree(ctx, p.layers);
     dfree(ctx, p.trees); dfree(ctx, p.xinv); dfree(ctx, p.pre_lo); dfree(ctx, p.pre_hi); dfree(ctx, p.wgmax);
     p = Plan();
 }
@@ -317,7 +328,8 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     fri_dist_detach(ctx);
     dfree(ctx, ctx->db.cyc); dfree(ctx, ctx->db.recv); dfree(ctx, ctx->db.half); dfree(ctx, ctx->db.roots);
     dfree(ctx, ctx->db.top); dfree(ctx, ctx->db.pre_lo); dfree(ctx, ctx->db.pre_hi); dfree(ctx, ctx->db.gath);
-    dfree(ctx, ctx->db.dq);
+    dfree(ctx, ctx->db.dq); dfree(ctx, ctx->db.rec); dfree(ctx, ctx->db.mx); dfree(ctx, ctx->db.c0);
+    dfree(ctx, ctx->db.sched);
     if (ctx->xstream) hipStreamDestroy(ctx->xstream);
     if (ctx->ev_vals) hipEventDestroy(ctx->ev_vals);
     if (ctx->ev_xchg) hipEventDestroy(ctx->ev_xchg);
@@ -731,6 +743,14 @@ static void plan_layout(Plan& p, size_t d, uint32_t log_n, uint32_t G, uint32_t 
     p.rank = rank;
     p.k_sw = sharded ? switch_layer(log_n, logG, p.rmax) : -1;
     const bool local_tail = sharded && p.k_sw < p.rmax;
+    // coefficient chunks: G * S_0 >= d, and S_k = S_0 / 2^k >= 1 up to k_sw
+    // (a pair 2j, 2j+1 of poly_{k-1} then never straddles two ranks' chunks)
+    p.cs0 = 0;
+    if (sharded) {
+        const size_t per = (d + G - 1) / G;
+        while (((size_t)1 << p.cs0) < per) p.cs0++;
+        if ((int)p.cs0 < p.k_sw) p.cs0 = (uint32_t)p.k_sw;
+    }
     std::vector<uint32_t> block_of(G), rank_of(G);
     for (uint32_t r = 0; r < G; r++) block_of[r] = rank_of[r] = r;
     lay = tre = xin = 0;
@@ -774,9 +794,20 @@ static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, u
     p.offset = offset;
     p.in_cap = d ? d : 1;
     p.coef_cap = d / 2 + 1;
+    p.coefF_cap = 0;
+    if (sharded) {
+        // chunks of poly_1 .. poly_k_sw, then the local tail's full poly_{k_sw+1} ..
+        const size_t S1 = p.cs0 >= 1 ? ((size_t)1 << (p.cs0 - 1)) : 1;
+        const size_t Ssw = (size_t)1 << (p.cs0 - (uint32_t)p.k_sw);
+        const bool local_tail = p.k_sw < p.rmax;
+        p.coef_cap = std::max(S1, local_tail ? G * Ssw / 2 : (size_t)0) + 1;
+        if (local_tail && p.k_sw >= 1) p.coefF_cap = G * Ssw;
+    }
     const size_t nhi = log_n > POW_LO_LOG ? ((size_t)1 << (log_n - POW_LO_LOG)) : 1;
     if (dalloc(ctx, &p.d_in, p.in_cap * 4) != hipSuccess || dalloc(ctx, &p.coefA, p.coef_cap * 4) != hipSuccess ||
-        dalloc(ctx, &p.coefB, p.coef_cap * 4) != hipSuccess || dalloc(ctx, &p.layers, lay * 4) != hipSuccess ||
+        dalloc(ctx, &p.coefB, p.coef_cap * 4) != hipSuccess ||
+        (p.coefF_cap && dalloc(ctx, &p.coefF, p.coefF_cap * 4) != hipSuccess) ||
+        dalloc(ctx, &p.layers, lay * 4) != hipSuccess ||
         dalloc(ctx, &p.trees, tre * 4) != hipSuccess || dalloc(ctx, &p.xinv, (xin ? xin : 1) * 4) != hipSuccess ||
         dalloc(ctx, &p.pre_lo, ((size_t)1 << POW_LO_LOG) * 4) != hipSuccess ||
         dalloc(ctx, &p.pre_hi, nhi * 4) != hipSuccess ||
@@ -1534,8 +1565,21 @@ static int sync_sharded(fri_ctx* ctx, hipStream_t s) {
                                     (drained ? ")" : "; stream still busy: destroy the context)"));
 }
 
+// Every transport call is logged (fri_debug_transport_log): chan 0 is the main
+// communicator on the context stream, 1 the exchange communicator on the
+// exchange stream, whatever stream the host transport actually uses.
+static void tp_log(fri_ctx* ctx, uint32_t chan, uint32_t op, int peer, size_t bytes) {
+    fri_transport_op e{};
+    e.chan = chan;
+    e.op = op;
+    e.peer = peer;
+    e.bytes = bytes;
+    if (ctx->tp.log.size() < 4096) ctx->tp.log.push_back(e);
+}
+
 static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
     Transport& tp = ctx->tp;
+    tp_log(ctx, 0, FRI_OP_ALLGATHER, -1, bytes);
     if (tp.loop) {
         for (int r = 0; r < tp.world; r++)
             FRI_HIP(ctx, hipMemcpyAsync((uint8_t*)drecv + (size_t)r * bytes, dsend, bytes, hipMemcpyDeviceToDevice, s));
@@ -1556,6 +1600,7 @@ static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t byt
 
 static int tp_alltoall(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes_per_peer, hipStream_t s) {
     Transport& tp = ctx->tp;
+    tp_log(ctx, 0, FRI_OP_ALLTOALL, -1, bytes_per_peer);
     if (tp.loop) {
         FRI_HIP(ctx, hipMemcpyAsync(drecv, dsend, bytes_per_peer * tp.world, hipMemcpyDeviceToDevice, s));
         return FRI_OK;
@@ -1587,14 +1632,17 @@ static int tp_alltoall(fri_ctx* ctx, const void* dsend, void* drecv, size_t byte
     return FRI_OK;
 }
 
-static int tp_sendrecv(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, int peer, hipStream_t s) {
+// chan 1: the exchange communicator (RCCL: on ctx->xstream, which `s` must be)
+static int tp_sendrecv(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, int peer, hipStream_t s,
+                       uint32_t chan) {
     Transport& tp = ctx->tp;
+    tp_log(ctx, chan, FRI_OP_SENDRECV, peer, bytes);
     if (tp.loop) {
         FRI_HIP(ctx, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, s));
         return FRI_OK;
     }
     if (!tp.host) {
-        ncclComm_t c = (s == ctx->xstream) ? tp.xcomm : tp.comm;
+        ncclComm_t c = chan ? tp.xcomm : tp.comm;
         FRI_NCCL(ctx, ncclGroupStart());
         FRI_NCCL(ctx, ncclSend(dsend, bytes, ncclUint8, peer, c, s));
         FRI_NCCL(ctx, ncclRecv(drecv, bytes, ncclUint8, peer, c, s));
@@ -1708,6 +1756,33 @@ extern "C" int fri_debug_attach_loopback(fri_ctx* ctx, int rank, int world) {
     return FRI_OK;
 }
 
+extern "C" int fri_debug_loopback_degrees(fri_ctx* ctx, const int32_t* deg, uint32_t n) {
+    if (!ctx) return FRI_EINVAL;
+    if (n > (uint32_t)MAXR + 1) return fail(ctx, FRI_EINVAL, "more degrees than layers");
+    ctx->db.sched_h.assign(deg ? deg : nullptr, deg ? deg + n : nullptr);
+    return FRI_OK;
+}
+
+extern "C" int fri_commit_degrees(fri_ctx* ctx, int32_t* out, size_t cap, uint32_t* n_out) {
+    if (!ctx || !n_out) return fail(ctx, FRI_EINVAL, "null argument");
+    settle(ctx);
+    const uint32_t n = ctx->h_state->n_layers;
+    *n_out = n;
+    if (n && (!out || cap < n)) return fail(ctx, FRI_EINVAL, "degree buffer too small (n_layers entries)");
+    for (uint32_t k = 0; k < n; k++) out[k] = ctx->h_state->deg[k];
+    return FRI_OK;
+}
+
+extern "C" int fri_debug_transport_log(fri_ctx* ctx, fri_transport_op* out, size_t cap, size_t* count) {
+    if (!ctx || !count) return fail(ctx, FRI_EINVAL, "null argument");
+    const auto& lg = ctx->tp.log;
+    *count = lg.size();
+    if (!out) return FRI_OK;                       // size query
+    if (cap < lg.size()) return fail(ctx, FRI_EINVAL, "log buffer too small (see count)");
+    for (size_t i = 0; i < lg.size(); i++) out[i] = lg[i];
+    return FRI_OK;
+}
+
 extern "C" int fri_dist_detach(fri_ctx* ctx) {
     if (!ctx) return FRI_EINVAL;
     Transport& tp = ctx->tp;
@@ -1753,6 +1828,7 @@ extern "C" int fri_dist_selftest(fri_ctx* ctx, size_t words_per_peer) {
     const size_t W = words_per_peer, tot = W * G;
     int rc = dist_buffers(ctx, tot, G, tot);
     if (rc) return rc;
+    ctx->tp.log.clear();
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     // read-backs land in pinned staging: a copy into pageable memory would
     // block the host behind a stalled collective before sync_sharded's deadline
@@ -1781,7 +1857,7 @@ extern "C" int fri_dist_selftest(fri_ctx* ctx, size_t words_per_peer) {
     // pair exchange on the exchange stream / split communicator, as the fold uses it
     FRI_HIP(ctx, hipEventRecord(ctx->ev_vals, s));
     FRI_HIP(ctx, hipStreamWaitEvent(ctx->xstream, ctx->ev_vals, 0));
-    if ((rc = tp_sendrecv(ctx, db.cyc, db.recv, tot * 4, (int)partner, ctx->tp.host ? s : ctx->xstream))) return rc;
+    if ((rc = tp_sendrecv(ctx, db.cyc, db.recv, tot * 4, (int)partner, ctx->tp.host ? s : ctx->xstream, 1))) return rc;
     FRI_HIP(ctx, hipEventRecord(ctx->ev_xchg, ctx->tp.host ? s : ctx->xstream));
     FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_xchg, 0));
     if ((rc = check("sendrecv", [&](uint32_t p, uint32_t i) { return (partner << 24) | (p << 16) | i; }))) return rc;
@@ -1806,6 +1882,12 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
         FRI_HIP(ctx, dalloc(ctx, &b.top, (size_t)(MAXR + 1) * 2 * 64 * 32));
         FRI_HIP(ctx, dalloc(ctx, &b.pre_lo, ((size_t)1 << POW_LO_LOG) * 4));
         FRI_HIP(ctx, dalloc(ctx, &b.pre_hi, nhi * 4));
+    }
+    if (!b.rec) {
+        FRI_HIP(ctx, dalloc(ctx, &b.rec, (size_t)(64 + 1) * REC_WORDS * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.mx, (size_t)64 * 3 * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.c0, 64));
+        FRI_HIP(ctx, dalloc(ctx, &b.sched, (size_t)(MAXR + 1) * 4));
     }
     if (b.gcap < gwords) {
         dfree(ctx, b.gath);
@@ -1859,6 +1941,12 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     rc = dist_buffers(ctx, M, G, (size_t)1 << (log_n - (uint32_t)p.k_sw));   // the layer gathered at the switch
     if (rc) return rc;
     DistBuf& db = ctx->db;
+    ctx->tp.log.clear();
+    if (ctx->tp.loop && !db.sched_h.empty()) {
+        std::vector<int32_t> sc(MAXR + 1, -1);
+        for (size_t i = 0; i < db.sched_h.size() && i <= (size_t)MAXR; i++) sc[i] = db.sched_h[i];
+        FRI_HIP(ctx, hipMemcpy(db.sched, sc.data(), sc.size() * 4, hipMemcpyHostToDevice));   // rehearsal only
+    }
     ctx->sharded_layers = (uint32_t)p.rmax + 1;      // lowered when the tail goes local
     init_state(ctx, ctx->h_sync, chan_in, flags, forced_betas);
     FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
@@ -1926,11 +2014,11 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
             if (!ctx->tp.host) {
                 FRI_HIP(ctx, hipEventRecord(ctx->ev_vals, s));
                 FRI_HIP(ctx, hipStreamWaitEvent(ctx->xstream, ctx->ev_vals, 0));
-                rc = tp_sendrecv(ctx, isA ? vals + B / 2 : vals, db.half, (B / 2) * 4, (int)partner, ctx->xstream);
+                rc = tp_sendrecv(ctx, isA ? vals + B / 2 : vals, db.half, (B / 2) * 4, (int)partner, ctx->xstream, 1);
                 if (rc) return rc;
                 FRI_HIP(ctx, hipEventRecord(ctx->ev_xchg, ctx->xstream));
             } else {
-                rc = tp_sendrecv(ctx, isA ? vals + B / 2 : vals, db.half, (B / 2) * 4, (int)partner, s);
+                rc = tp_sendrecv(ctx, isA ? vals + B / 2 : vals, db.half, (B / 2) * 4, (int)partner, s, 1);
                 if (rc) return rc;
             }
         }
@@ -1946,17 +2034,24 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         size_t spl = (k == 0 && tl.L >= 19) ? span_begin(ctx, "merkle_layer0_leaf", ((uint64_t)4 << tl.L) + 32 * leaf_nodes)
                                             : (size_t)-1;
         size_t spk = span_begin(ctx, k == 0 ? "layer0" : "layers", 0);
-        // coefficient task of this layer (redundant on every rank; needs only
-        // round k-1's beta): on its own stream, concurrent with the block tree
+        // coefficient task of this layer, sharded (next_fri_polynomial,
+        // fri_commit.rs:32-50): this rank folds coefficients [rank*S_k,
+        // (rank+1)*S_k) of poly_k (k == 0: scans that range of the input) into
+        // its chunk buffer, on its own stream, concurrent with the block tree.
+        // It needs only round k-1's beta and degree (replicated DevState).
+        const size_t Sk = (size_t)1 << (p.cs0 - (uint32_t)k);
         LayerTask tc{};
         tc.k = k;
-        tc.coef_in = k ? coef_buf(p, k - 1) : p.d_in;
+        tc.coef_in = (k <= 1) ? p.d_in : coef_buf(p, k - 1);
+        tc.ibase = (k <= 1) ? 0 : (size_t)rank * (Sk << 1);
         tc.coef_out = k ? coef_buf(p, k) : nullptr;
+        tc.obase = (size_t)rank * Sk;
+        tc.jlo = (size_t)rank * Sk;
+        tc.jhi = (size_t)(rank + 1) * Sk;
         tc.d0 = d;
         tc.wgmax = p.wgmax;
         tc.st = ctx->d_state;
-        const size_t clen = k ? ((d + ((size_t)1 << k) - 1) >> k) : d;
-        uint32_t Gc = (uint32_t)((clen + 8191) / 8192);
+        uint32_t Gc = (uint32_t)((Sk + 8191) / 8192);
         if (Gc < 1) Gc = 1;
         if (Gc > 2048) Gc = 2048;
         const bool side = !ctx->profiling;   // (profiled commits keep one stream for the spans)
@@ -1976,17 +2071,24 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
             launch_coef(tc, Gc, ctx->cstream);
             FRI_HIP(ctx, hipEventRecord(ctx->ev_coef, ctx->cstream));
         }
-        // all-gather block roots -> block order -> top tree level 0
-        rc = tp_allgather(ctx, tl.tree + 8 * level_offset(tl.L, tl.L), db.roots, 32, s);
-        if (rc) return rc;
-        uint32_t* top = db.top + (size_t)k * 2 * 64 * 8;
-        launch_permute_digests(db.roots, top, G, block_of.data(), s);
+        // this rank's record (block root, maxima of its coefficient slice, its
+        // first coefficient) -> all-gather -> top tree level 0 in block order,
+        // the G maxima triples and the final-value candidate of rank 0
         if (side) FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_coef, 0));
         else launch_coef(tc, Gc, s);
+        const int gate = k > 0 ? k - 1 : -1;
+        launch_shard_record(tl.tree + 8 * level_offset(tl.L, tl.L), p.wgmax, Gc, k ? tc.coef_out : p.d_in, db.rec,
+                            ctx->d_state, gate, s);
+        rc = tp_allgather(ctx, db.rec, db.rec + REC_WORDS, REC_WORDS * 4, s);
+        if (rc) return rc;
+        uint32_t* top = db.top + (size_t)k * 2 * 64 * 8;
+        launch_shard_unpack(db.rec + REC_WORDS, G, block_of.data(), 0u, top, db.mx, db.c0,
+                            (ctx->tp.loop && !db.sched_h.empty()) ? db.sched : nullptr, k, ctx->d_state, gate, s);
         LayerTask tt = tc;
         tt.tree = top;
         tt.L = logG;
-        launch_top(tt, 0, p.wgmax, Gc, s);
+        tt.coef_in = tt.coef_out = db.c0;    // k_tree_top's final value: poly_k[0] (rank 0's chunk)
+        launch_top(tt, 0, db.mx, G, s);
         span_end(ctx, spk);
         if (last) break;
         if (next_sharded) {
@@ -2003,9 +2105,22 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         }
         // switch to local: gather layer k in block order, then the 1-GPU pipeline from k+1
         ctx->sharded_layers = (uint32_t)k + 1;   // layer k keeps its block-local tree; k+1.. are local
-        sp = span_begin(ctx, "gather", B * 4 * G);
+        sp = span_begin(ctx, "gather", B * 4 * G + Sk * 4 * G);
         rc = tp_allgather(ctx, vals, db.gath, B * 4, s);
         if (rc) return rc;
+        // poly_k whole for the local coefficient fold (chunks in rank order
+        // are poly_k in coefficient order); at k == 0 every rank has the input
+        if (k >= 1) {
+            if (p.coefF_cap < G * Sk) return fail(ctx, FRI_ESTATE, "shard plan out of step (coefficient gather)");
+            rc = tp_allgather(ctx, tc.coef_out, p.coefF, Sk * 4, s);
+            if (rc) return rc;
+        }
+        // layer kk of the local tail; the first one folds the gathered poly_k
+        auto tail_task = [&](int kk) {
+            LayerTask t = commit_task(ctx, kk);
+            if (kk == k + 1 && k >= 1) t.coef_in = p.coefF;
+            return t;
+        };
         // the gathered blocks into place and the local layers: the same
         // launches on every commit of this plan (block_of at the switch is
         // fixed by (G, rank)), so they replay as one hipGraph captured on the
@@ -2018,11 +2133,11 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
                 if (log_n - (uint32_t)kk <= TAIL_LOG) {      // small layers: one launch
                     LayerTask ts[TAIL_LOG + 1];
                     uint32_t nt = 0;
-                    for (int k2 = kk; k2 <= p.rmax; k2++) ts[nt++] = commit_task(ctx, k2);
+                    for (int k2 = kk; k2 <= p.rmax; k2++) ts[nt++] = tail_task(k2);
                     launch_tail(ts, nt, s);
                     break;
                 }
-                launch_layer(commit_task(ctx, kk), s);
+                launch_layer(tail_task(kk), s);
             }
             return FRI_OK;
         };
@@ -2107,6 +2222,7 @@ extern "C" int fri_decommit_query_sharded(fri_ctx* ctx, uint64_t index, uint32_t
     DistBuf& db = ctx->db;
     constexpr size_t SLOT = 16384;                          // words per rank slot (64 KiB)
     if (!db.dq) FRI_HIP(ctx, dalloc(ctx, &db.dq, (size_t)(64 + 1) * SLOT * 4));
+    ctx->tp.log.clear();
     int rc = tp_host_stage(ctx, G * SLOT * 4);
     if (rc) return rc;
     hipStream_t s = ctx->stream;

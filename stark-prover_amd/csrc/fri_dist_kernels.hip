@@ -109,4 +109,65 @@ void launch_permute_digests(const uint32_t* src, uint32_t* dst, uint32_t G, cons
     hipLaunchKernelGGL(k_permute_digests, dim3(1), dim3(512), 0, s, src, dst, G, pm);
 }
 
+// Per-layer record of one rank (REC_WORDS words, all-gathered): its block
+// root, the maxima (m0, m1, m2) of its slice of the coefficient task
+// (reduced from the R workgroup triples) and its poly_k coefficient obase
+// (the final value when rank 0's chunk starts at 0 and deg_k == 0).
+// One wave; gated like the layer it belongs to.
+__global__ void k_shard_record(const uint32_t* __restrict__ root, const int32_t* __restrict__ wgmax, uint32_t R,
+                               const uint32_t* __restrict__ c0, uint32_t* __restrict__ rec, const DevState* st,
+                               int gate) {
+    if (gate >= 0 && !st->active[gate]) return;
+    const uint32_t t = threadIdx.x;
+    int a = -1, b = -1, c = -1;
+    for (uint32_t i = t; i < R; i += 64) {
+        a = max(a, wgmax[3 * i]); b = max(b, wgmax[3 * i + 1]); c = max(c, wgmax[3 * i + 2]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a = max(a, __shfl_xor(a, off)); b = max(b, __shfl_xor(b, off)); c = max(c, __shfl_xor(c, off));
+    }
+    if (t < 8) rec[t] = root[t];
+    if (t == 0) {
+        rec[8] = (uint32_t)a; rec[9] = (uint32_t)b; rec[10] = (uint32_t)c;
+        rec[11] = c0 ? c0[0] : 0u;
+        rec[12] = rec[13] = rec[14] = rec[15] = 0u;
+    }
+}
+void launch_shard_record(const uint32_t* root, const int32_t* wgmax, uint32_t R, const uint32_t* c0, uint32_t* rec,
+                         const DevState* st, int gate, hipStream_t s) {
+    hipLaunchKernelGGL(k_shard_record, dim3(1), dim3(64), 0, s, root, wgmax, R, c0, rec, st, gate);
+}
+
+// The G all-gathered records (rank order) -> the top tree's level 0 in block
+// order, the G maxima triples for k_tree_top (mx[3r..3r+2]) and the final
+// value candidate from the rank holding coefficient 0 (c0out).  sched
+// (loopback rehearsal only): the recorded degree of every layer replaces the
+// maxima, so one rank's share runs every round of the real commit.
+__global__ void k_shard_unpack(const uint32_t* __restrict__ recs, uint32_t G, Perm64 pm, uint32_t c0_rank,
+                               uint32_t* __restrict__ top, int32_t* __restrict__ mx, uint32_t* __restrict__ c0out,
+                               const int32_t* __restrict__ sched, int k, const DevState* st, int gate) {
+    if (gate >= 0 && !st->active[gate]) return;
+    const uint32_t i = threadIdx.x;
+    if (i < G * 8) {
+        const uint32_t r = i / 8, w = i % 8;
+        top[8 * pm.p[r] + w] = recs[REC_WORDS * r + w];
+    }
+    if (i < G * 3) {
+        const uint32_t r = i / 3, j = i % 3;
+        int32_t v = (int32_t)recs[REC_WORDS * r + 8 + j];
+        if (sched) v = j == 0 ? sched[k] : j == 1 ? (k == 0 ? -1 : 0) : -1;   // k = 0: deg = m0, canonical
+        mx[i] = v;
+    }
+    if (i == 0) c0out[0] = recs[REC_WORDS * c0_rank + 11];
+}
+void launch_shard_unpack(const uint32_t* recs, uint32_t G, const uint32_t* block_of_rank, uint32_t c0_rank,
+                         uint32_t* top, int32_t* mx, uint32_t* c0out, const int32_t* sched, int k, const DevState* st,
+                         int gate, hipStream_t s) {
+    Perm64 pm{};
+    for (uint32_t r = 0; r < G && r < 64; r++) pm.p[r] = block_of_rank[r];
+    hipLaunchKernelGGL(k_shard_unpack, dim3(1), dim3(512), 0, s, recs, G, pm, c0_rank, top, mx, c0out, sched, k, st,
+                       gate);
+}
+
 }  // namespace fri

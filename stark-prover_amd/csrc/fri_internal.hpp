@@ -129,6 +129,11 @@ struct LayerTask {
     DevState* st;              // nullptr: standalone Merkle tree (no degree / channel)
     const DevState* gst;       // gate for standalone trees inside a commit (sharded
     int gidx;                  //   layers): skip when !gst->active[gidx]
+    // Sharded coefficient fold (run_commit_sharded, k_coef only): this rank
+    // handles the coefficients j in [jlo, jhi) of poly_k (jhi == 0: all of
+    // them); coef_in[0] holds global coefficient ibase of poly_{k-1} (of the
+    // input at k == 0), coef_out[0] global coefficient obase of poly_k.
+    size_t jlo, jhi, ibase, obase;
 };
 void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end = nullptr);
 // Layers ts[0..n) (consecutive, 2^L <= 2^TAIL_LOG elements, commit mode) in
@@ -147,6 +152,16 @@ void launch_pair_fold(const uint32_t* first, const uint32_t* second, const uint3
                       const DevState* st, int r, hipStream_t s);
 void launch_permute_digests(const uint32_t* src, uint32_t* dst, uint32_t G, const uint32_t* block_of_rank,
                             hipStream_t s);
+// Sharded coefficient fold: the per-layer record each rank all-gathers
+// (block root, maxima of its coefficient slice, its first coefficient) and
+// its unpacking on every rank (top level 0 in block order, G maxima triples,
+// the final-value candidate).
+constexpr uint32_t REC_WORDS = 16;
+void launch_shard_record(const uint32_t* root, const int32_t* wgmax, uint32_t R, const uint32_t* c0, uint32_t* rec,
+                         const DevState* st, int gate, hipStream_t s);
+void launch_shard_unpack(const uint32_t* recs, uint32_t G, const uint32_t* block_of_rank, uint32_t c0_rank,
+                         uint32_t* top, int32_t* mx, uint32_t* c0out, const int32_t* sched, int k, const DevState* st,
+                         int gate, hipStream_t s);
 // Tree top + degree + channel step for a layer whose level `l` (2^(L-l)
 // nodes, <= 512) is already in t.tree; mx/G: coefficient maxima.
 void launch_top(const LayerTask& t, uint32_t l, const int32_t* mx, uint32_t G, hipStream_t s);

@@ -119,12 +119,17 @@ __device__ __forceinline__ int wave_max_i(int v) {
 // maxima of c', even part, odd part.  Results: wgmax[3w .. 3w+2].
 __device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red /*LDS [3*waves]*/) {
     int m0 = -1, m1 = -1, m2 = -1;
+    // this rank's coefficient range (all of poly_k unless sharded), split
+    // evenly over the G workgroups; indices j are global
+    const size_t jhi_all = t.jhi ? t.jhi : ~(size_t)0;
     if (t.k == 0) {
         // m1 >= 0 flags a coefficient >= p (the input is validated here, on
         // the device, instead of by a host scan before the upload)
-        const size_t n = t.d0, cs = (n + G - 1) / G, lo = (size_t)w * cs, hi = min(n, lo + cs);
+        const size_t a = t.jlo, b = min(t.d0, jhi_all), n = b > a ? b - a : 0;
+        const size_t cs = (n + G - 1) / G, lo = a + (size_t)w * cs, hi = min(b, lo + cs);
+        const uint32_t* in = t.coef_in - t.ibase;
         for (size_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
-            const uint32_t c = t.coef_in[j];
+            const uint32_t c = in[j];
             if (c) m0 = max(m0, (int)j);
             if (c >= P) m1 = 0;
         }
@@ -132,12 +137,15 @@ __device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32
         const DevState* st = t.st;
         const size_t len = (size_t)(st->deg[t.k - 1] + 1), nlen = (len + 1) / 2;
         const uint32_t beta_m = st->beta_mont[t.k - 1];
-        const size_t cs = (nlen + G - 1) / G, lo = (size_t)w * cs, hi = min(nlen, lo + cs);
+        const size_t a = t.jlo, b = min(nlen, jhi_all), n = b > a ? b - a : 0;
+        const size_t cs = (n + G - 1) / G, lo = a + (size_t)w * cs, hi = min(b, lo + cs);
+        const uint32_t* in = t.coef_in - t.ibase;
+        uint32_t* outp = t.coef_out - t.obase;
         for (size_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
-            uint32_t e = t.coef_in[2 * j];
-            uint32_t o = (2 * j + 1 < len) ? t.coef_in[2 * j + 1] : 0u;
+            uint32_t e = in[2 * j];
+            uint32_t o = (2 * j + 1 < len) ? in[2 * j + 1] : 0u;
             uint32_t v = add(e, mmul(o, beta_m));
-            t.coef_out[j] = v;
+            outp[j] = v;
             if (v) m0 = (int)j;
             if (e) m1 = (int)j;
             if (o) m2 = (int)j;

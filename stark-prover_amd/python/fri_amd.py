@@ -69,6 +69,14 @@ class Collectives(ctypes.Structure):
                                               ctypes.c_size_t, ctypes.c_int))]
 
 
+class TransportOp(ctypes.Structure):
+    """fri_transport_op: one entry of fri_debug_transport_log."""
+    _fields_ = [("chan", ctypes.c_uint32), ("op", ctypes.c_uint32), ("peer", ctypes.c_int32),
+                ("reserved", ctypes.c_uint32), ("bytes", ctypes.c_uint64)]
+
+
+TRANSPORT_OPS = {1: "allgather", 2: "alltoall", 3: "sendrecv"}
+
 _lib = None
 
 
@@ -136,6 +144,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                             ctypes.POINTER(CommitResult)]),
         "fri_decommit_query_sharded": (i32, [vp, ctypes.c_uint64, pu32, sz, ctypes.c_char_p, sz,
                                              ctypes.POINTER(sz)]),
+        "fri_debug_loopback_degrees": (i32, [vp, ctypes.POINTER(ctypes.c_int32), u32]),
+        "fri_commit_degrees": (i32, [vp, ctypes.POINTER(ctypes.c_int32), sz, ctypes.POINTER(u32)]),
+        "fri_debug_transport_log": (i32, [vp, ctypes.POINTER(TransportOp), sz, ctypes.POINTER(sz)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -468,6 +479,33 @@ class Context:
         """Timing rehearsal (fri_debug_attach_loopback): collectives return
         this rank's own bytes; the transcript is not the real one."""
         self._check(self.lib.fri_debug_attach_loopback(self.h, rank, world))
+
+    def loopback_degrees(self, degrees: Optional[Sequence[int]]):
+        """The rehearsal's degree schedule (fri_debug_loopback_degrees): the
+        per-layer degrees of a 1-GPU commit of the same polynomial
+        (commit_degrees), so the rehearsal runs every round of the real
+        commit although the coefficient fold is sharded. None clears it."""
+        if not degrees:
+            self._check(self.lib.fri_debug_loopback_degrees(self.h, None, 0))
+            return
+        a = (ctypes.c_int32 * len(degrees))(*[int(x) for x in degrees])
+        self._check(self.lib.fri_debug_loopback_degrees(self.h, a, len(degrees)))
+
+    def commit_degrees(self) -> List[int]:
+        """deg(poly_k) of every layer of the resident commit (fri_commit_degrees)."""
+        n = ctypes.c_uint32()
+        buf = (ctypes.c_int32 * (MAX_ROUNDS + 1))()
+        self._check(self.lib.fri_commit_degrees(self.h, buf, MAX_ROUNDS + 1, ctypes.byref(n)))
+        return [int(buf[i]) for i in range(n.value)]
+
+    def transport_log(self) -> List[tuple]:
+        """(chan, op, peer, bytes) of every collective of the last sharded call
+        (fri_debug_transport_log); op is "allgather", "alltoall" or "sendrecv"."""
+        cnt = ctypes.c_size_t()
+        self._check(self.lib.fri_debug_transport_log(self.h, None, 0, ctypes.byref(cnt)))
+        buf = (TransportOp * max(1, cnt.value))()
+        self._check(self.lib.fri_debug_transport_log(self.h, buf, cnt.value, ctypes.byref(cnt)))
+        return [(e.chan, TRANSPORT_OPS[e.op], e.peer, e.bytes) for e in buf[:cnt.value]]
 
     def detach(self):
         self._check(self.lib.fri_dist_detach(self.h))

@@ -23,9 +23,36 @@ sys.path.insert(0, os.path.join(ROOT, "stark-prover_amd", "python"))
 sys.path.insert(0, HERE)
 
 
+def make_coeffs(kind, seed, d):
+    """Coefficient vectors of the multi-rank tests (numpy uint32).  Beyond
+    random full-degree polynomials they steer the sharded degree bookkeeping
+    (next_fri_polynomial, fri_commit.rs:32-50) through its other branches:
+      odd_only   every even coefficient zero: round 1 takes add_assign's early
+                 return (the degree of beta*odd, untrimmed);
+      low_degree only the first 3 coefficients nonzero (degree 2, two rounds):
+                 the commit ends while the layers are still sharded, and the
+                 final value comes from the rank holding coefficient 0;
+      tail_heavy the top coefficient nonzero, a zero run below it: the degree
+                 maxima come from the last rank's chunk."""
+    import numpy as np
+
+    import fri_oracle as fo
+    c = fo.splitmix64_np(seed, d).astype(np.uint32)
+    if kind == "odd_only":
+        c[0::2] = 0
+    elif kind == "low_degree":
+        c[3:] = 0
+    elif kind == "tail_heavy":
+        c[d // 3:d - 1] = 0
+    elif kind != "random":
+        raise ValueError(kind)
+    return c
+
+
 def main():
     mode, log_n, seed, out_dir = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     blowup_log = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+    kind = os.environ.get("POLY_KIND", "random")
     import torch.distributed as dist
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -33,7 +60,9 @@ def main():
 
     import fri_oracle as fo
     d = (1 << log_n) >> blowup_log
-    coeffs = fo.splitmix64_np(seed, d) if mode == "gpu_shard" else fo.splitmix64_field(seed, d)
+    coeffs = make_coeffs(kind, seed, d)
+    if mode == "model":
+        coeffs = [int(x) for x in coeffs]
     if mode == "gpu_shard":
         import time
         import fri_amd
@@ -43,12 +72,14 @@ def main():
         ctx.attach_torch(rank, world)
         ctx.dist_selftest(1024)
         r = ctx.commit_sharded(coeffs, log_n)
+        tlog = ctx.transport_log()
         cur, peak = ctx.device_bytes()
         res = {"roots": [bytes(r.roots[k]).hex() for k in range(r.n_layers)],
                "betas": [int(r.betas[i]) for i in range(r.n_rounds)],
                "final_value": int(r.final_value), "final_degree": int(r.final_degree),
                "state": bytes(r.channel_out.digest).hex(), "hbm_bytes": cur, "hbm_peak_bytes": peak,
-               "ctx_log_n_max": log_n - logw, "seconds": round(time.monotonic() - t0, 2)}
+               "ctx_log_n_max": log_n - logw, "seconds": round(time.monotonic() - t0, 2),
+               "transport_log": tlog}
         try:
             ctx.layer(0, log_n)
             res["layer0_refused"] = False
@@ -77,7 +108,7 @@ def main():
         ctx.dist_selftest(1024)
         # a coefficient >= p: rejected on the device by every rank (layer 0's
         # replicated top), after the collectives ran in step on all ranks
-        bad = np.asarray(coeffs, dtype=np.uint32)
+        bad = np.array(coeffs, dtype=np.uint32)      # a copy: coeffs stays canonical
         bad[len(bad) // 3] = fo.P
         try:
             ctx.commit_sharded(bad, log_n)
@@ -85,7 +116,9 @@ def main():
         except fri_amd.FriError as e:
             rejected = e.code == fri_amd.FRI_EINVAL
         r = ctx.commit_sharded(coeffs, log_n)
-        res = {"noncanonical_rejected": rejected, "roots": [bytes(r.roots[k]).hex() for k in range(r.n_layers)],
+        tlog = ctx.transport_log()
+        res = {"noncanonical_rejected": rejected, "transport_log": tlog,
+               "roots": [bytes(r.roots[k]).hex() for k in range(r.n_layers)],
                "betas": [int(r.betas[i]) for i in range(r.n_rounds)],
                "final_value": int(r.final_value), "final_degree": int(r.final_degree),
                "state": bytes(r.channel_out.digest).hex()}
@@ -96,16 +129,24 @@ def main():
         except fri_amd.FriError:
             res["layer0_refused"] = True
         last = r.n_layers - 1
-        tail = ctx.layer(last, log_n)
-        qi = min(1, tail.size - 1)            # a 1-element last layer (blowup 1) has only index 0
-        _, path = ctx.auth_path(last, qi, log_n)
+        try:
+            tail = ctx.layer(last, log_n)
+        except fri_amd.FriError as e:          # the commit ended inside the sharded layers
+            assert e.code == fri_amd.FRI_ESTATE and kind == "low_degree", e
+            tail = None
+        if tail is not None:
+            qi = min(1, tail.size - 1)        # a 1-element last layer (blowup 1) has only index 0
+            _, path = ctx.auth_path(last, qi, log_n)
         qidx = [0, 1, (1 << log_n) - 1, 0x9E3779B97F4A7C15 % (1 << log_n)]
         dq_sharded = [ctx.decommit_query(i, r.n_layers, log_n, sharded=True) for i in qidx]
         ctx.detach()
         single = ctx.commit(coeffs, log_n)
         res["decommit_matches_single"] = dq_sharded == [ctx.decommit_query(i, single.n_layers, log_n) for i in qidx]
-        res["tail_matches_single"] = bool(np.array_equal(tail, ctx.layer(last, log_n)))
-        res["auth_matches_single"] = path == ctx.auth_path(last, qi, log_n)[1]
+        if tail is None:                      # nothing local to compare: the decommitment covers the layers
+            res["tail_matches_single"] = res["auth_matches_single"] = "sharded"
+        else:
+            res["tail_matches_single"] = bool(np.array_equal(tail, ctx.layer(last, log_n)))
+            res["auth_matches_single"] = path == ctx.auth_path(last, qi, log_n)[1]
         res["single_root0"] = bytes(single.roots[0]).hex()
         ctx.close()
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
@@ -115,4 +156,12 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:
+        # the test reads this file: torchrun's own summary hides the traceback
+        import traceback
+        rank = os.environ.get("RANK", "x")
+        with open(os.path.join(sys.argv[4], f"rank{rank}.err"), "w") as f:
+            f.write(traceback.format_exc())
+        raise

@@ -24,53 +24,104 @@ def free_port():
     return p
 
 
-def run_ranks(mode, world, log_n, seed, timeout, env_extra=None, blowup_log=3, stream_stderr=False):
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from dist_worker import make_coeffs  # noqa: E402
+
+
+def run_ranks(mode, world, log_n, seed, timeout, env_extra=None, blowup_log=3, stream_stderr=False, kind="random"):
     out = tempfile.mkdtemp(prefix=f"fri_{mode}_")
     env = dict(os.environ)
     env["MASTER_ADDR"] = "127.0.0.1"
+    env["POLY_KIND"] = kind
     env.update(env_extra or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "dist_worker.py"), mode, str(log_n), str(seed), out, str(blowup_log)]
     r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None if stream_stderr else subprocess.PIPE,
                        text=True, timeout=timeout)
-    assert r.returncode == 0, (r.stderr or "")[-3000:]
+    if r.returncode != 0:
+        errs = "".join(open(os.path.join(out, f)).read() for f in sorted(os.listdir(out)) if f.endswith(".err"))
+        raise AssertionError(f"ranks failed:\n{errs[-6000:]}\n--- stderr tail ---\n{(r.stderr or '')[-2000:]}")
     res = [json.load(open(os.path.join(out, f"rank{i}.json"))) for i in range(world)]
     return res
 
 
-def single_node(oracle, log_n, seed):
-    coeffs = oracle.splitmix64_field(seed, (1 << log_n) // 8)
+def single_node(oracle, log_n, seed, kind="random"):
+    coeffs = [int(x) for x in make_coeffs(kind, seed, (1 << log_n) // 8)]
     ch = oracle.Channel()
     r = oracle.fri_commit(coeffs, log_n, ch, keep=False)
     return {"roots": [x.hex() for x in r.roots], "betas": r.betas, "final_value": r.final_value,
             "final_degree": r.final_degree, "state": ch.state}
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_sharded_protocol_model_gloo(oracle, world):
+def check_transport_schedule(logs):
+    """The RCCL deadlock-freedom condition on the logged
+    schedules of every rank (fri_debug_transport_log): per channel (0: main
+    communicator, 1: exchange communicator) every rank issues the same
+    sequence of (op, bytes), and every pair exchange at position i with peer q
+    is matched by q's pair exchange at position i with this rank as peer."""
+    world = len(logs)
+    for chan in (0, 1):
+        seqs = [[tuple(e) for e in lg if e[0] == chan] for lg in logs]
+        assert len({len(q) for q in seqs}) == 1, f"chan {chan}: ranks issue different numbers of collectives"
+        for i in range(len(seqs[0])):
+            assert len({(q[i][1], q[i][3]) for q in seqs}) == 1, f"chan {chan} position {i}: {[q[i] for q in seqs]}"
+            if seqs[0][i][1] == "sendrecv":
+                for r in range(world):
+                    peer = seqs[r][i][2]
+                    assert 0 <= peer < world and peer != r
+                    assert seqs[peer][i][2] == r, f"chan {chan} position {i}: rank {r} -> {peer} unmatched"
+            else:
+                assert all(q[i][2] == -1 for q in seqs)
+    return [len([e for e in logs[0] if e[0] == c]) for c in (0, 1)]
+
+
+@pytest.mark.parametrize("world,kind", [(2, "random"), (4, "random"), (8, "random"),
+                                        (4, "odd_only"), (8, "odd_only"), (4, "low_degree"),
+                                        (8, "low_degree"), (4, "tail_heavy")])
+def test_sharded_protocol_model_gloo(oracle, world, kind):
+    """The sharded protocol, the sharded coefficient fold and its degree
+    records included, modelled over gloo with the C oracle doing the per-block
+    work: the transcript equals the single-node oracle's."""
     log_n = 10
-    want = single_node(oracle, log_n, 42)
-    got = run_ranks("model", world, log_n, 42, timeout=600, env_extra={"SHARD_MIN": "7"})
+    want = single_node(oracle, log_n, 42, kind)
+    got = run_ranks("model", world, log_n, 42, timeout=600, env_extra={"SHARD_MIN": "7"}, kind=kind)
     for r in got:
         assert r == want
 
 
+def test_transport_schedule_check_rejects_mismatch():
+    """The schedule check itself: a reordered collective, a size mismatch and
+    an unmatched pair exchange are each caught."""
+    ok = [[(0, "alltoall", -1, 64), (1, "sendrecv", 1, 32), (0, "allgather", -1, 64)],
+          [(0, "alltoall", -1, 64), (1, "sendrecv", 0, 32), (0, "allgather", -1, 64)]]
+    assert check_transport_schedule(ok) == [2, 1]
+    bad_order = [ok[0], [ok[1][2], ok[1][1], ok[1][0]]]
+    bad_size = [ok[0], [ok[1][0], (1, "sendrecv", 0, 16), ok[1][2]]]
+    bad_peer = [[(1, "sendrecv", 1, 8)], [(1, "sendrecv", 1, 8)]]
+    for bad in (bad_order, bad_size, bad_peer):
+        with pytest.raises(AssertionError):
+            check_transport_schedule(bad)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,log_n,blowup_log", [
-    (2, 22, 3), (4, 22, 3),          # several sharded layers, then local
-    (2, 20, 3), (2, 21, 3),          # switch to local right after layer 0 / 1
-    (2, 21, 1), (4, 22, 0),          # d > n/G: the coset reduction folds several chunks
-    (8, 23, 3),                      # the driver's N = 8 shape: 3-level top, block permutations
+@pytest.mark.parametrize("world,log_n,blowup_log,kind", [
+    (2, 22, 3, "random"), (4, 22, 3, "random"),    # several sharded layers, then local
+    (2, 20, 3, "random"), (2, 21, 3, "random"),    # switch to local right after layer 0 / 1
+    (2, 21, 1, "random"), (4, 22, 0, "random"),    # d > n/G: the coset reduction folds several chunks
+    (8, 23, 3, "random"),                          # the driver's N = 8 shape: 3-level top, block permutations
+    (4, 22, 3, "odd_only"),                        # add_assign's early return in a sharded round
+    (8, 23, 3, "low_degree"),                      # the commit ends in a sharded layer (final value: rank 0)
+    (4, 22, 3, "tail_heavy"),                      # the degree comes from the last rank's chunk
 ])
-def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, corc, oracle):
+def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, kind, corc, oracle):
     import ctypes
 
     import numpy as np
     seed = 7
-    got = run_ranks("gpu", world, log_n, seed, timeout=900, blowup_log=blowup_log)
+    got = run_ranks("gpu", world, log_n, seed, timeout=900, blowup_log=blowup_log, kind=kind)
     d = (1 << log_n) >> blowup_log
-    c = np.ascontiguousarray(np.array(oracle.splitmix64_field(seed, d), dtype=np.uint64))
+    c = np.ascontiguousarray(make_coeffs(kind, seed, d).astype(np.uint64))
     och = oracle.OrcChannel()
     corc.orc_channel_init(ctypes.byref(och))
     ores = oracle.OrcFriResult()
@@ -83,9 +134,13 @@ def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, corc, oracl
         assert r["final_value"] == ores.final_value
         assert r["state"] == och.state.decode()
         assert r["layer0_refused"] and r["tail_matches_single"] and r["auth_matches_single"]
+        if kind != "low_degree":
+            assert r["tail_matches_single"] is True and r["auth_matches_single"] is True
         assert r["decommit_matches_single"]
         assert r["noncanonical_rejected"]
         assert r["single_root0"] == want_roots[0]
+    n_main, n_x = check_transport_schedule([r["transport_log"] for r in got])
+    assert n_main >= 1 and (n_x >= 1 or kind == "low_degree" or log_n - 1 < 20)
 
 
 @pytest.mark.gpu
@@ -99,12 +154,23 @@ def test_loopback_rehearsal_transport(oracle):
     import numpy as np
     log_n, world = 22, 8
     c = oracle.splitmix64_np(11, (1 << log_n) >> 3).astype(np.uint32)
+    one = fri_amd.Context(0, log_n)
+    try:
+        ref = one.commit(c, log_n)
+        degrees = one.commit_degrees()
+    finally:
+        one.close()
+    assert len(degrees) == ref.n_layers and degrees[0] == c.size - 1 and degrees[-1] == 0
     ctx = fri_amd.Context(0, log_n - 3)
     try:
-        ctx.attach_loopback(3, world)
-        assert ctx.dist_info() == (3, world, "loopback")
+        ctx.attach_loopback(0, world)
+        assert ctx.dist_info() == (0, world, "loopback")
+        ctx.loopback_degrees(degrees)
         r = ctx.commit_sharded(c, log_n)
-        assert (r.n_layers, r.n_rounds) == (log_n - 2, log_n - 3)
+        assert (r.n_layers, r.n_rounds) == (ref.n_layers, ref.n_rounds) == (log_n - 2, log_n - 3)
+        assert ctx.commit_degrees() == degrees
+        ops = [e[1] for e in ctx.transport_log()]
+        assert ops.count("alltoall") == 1 and "sendrecv" in ops
         ctx.detach()
         assert ctx.dist_info()[2] == "none"
         with pytest.raises(fri_amd.FriError) as e:
@@ -227,6 +293,7 @@ def test_sharded_2p28_world8_configs4(oracle_commit):
     the channel state equal the OpenMP C oracle's 1-node commit, on every rank,
     and each rank holds well under 1/8 of the ~38 GB a 1-GPU 2^28 commit needs."""
     got = run_ranks("gpu_shard", 8, 28, 8, timeout=1100, stream_stderr=True)
+    check_transport_schedule([r["transport_log"] for r in got])
     want = oracle_commit(28, 8)
     for r in got:
         assert r["roots"] == want["roots"]
@@ -249,10 +316,14 @@ def test_sharded_shard_sized_context(world, log_n, blowup_log, oracle_commit):
     as the oracle, and per-rank HBM well below what the whole-codeword plan
     needed (layers + trees alone are ~130 * 2^log_n bytes)."""
     got = run_ranks("gpu_shard", world, log_n, 11, timeout=900, blowup_log=blowup_log)
+    check_transport_schedule([r["transport_log"] for r in got])
     want = oracle_commit(log_n, 11, blowup_log)
+    d = (1 << log_n) >> blowup_log
     for r in got:
         assert {k: r[k] for k in want} == want
         assert r["layer0_refused"] and r["last_layer_constant"]
         assert r["verify_fri"] and r["transcript_sha"] == got[0]["transcript_sha"]
-        d_bytes = 8 * ((1 << log_n) >> blowup_log)     # input + coefficient-fold buffers, full on every rank
+        # the input (full: the coset LDE reads it) and the coefficient-fold
+        # chunks (two buffers of d / (2 world) words, or the local tail's poly)
+        d_bytes = 4 * d + 8 * max(d // (2 * world), d >> 9)
         assert r["hbm_peak_bytes"] < 130 * (1 << log_n) / world + d_bytes + (512 << 20), r["hbm_peak_bytes"]

@@ -11,8 +11,11 @@ returns this rank's own bytes as a device-to-device copy on the stream RCCL
 would use, so the GPU never idles on a host round trip.  The transcript is
 NOT the real one (the run is not checked), but every kernel the rank would
 launch runs, on data of the right shape.
-The degree progression comes from the replicated coefficient fold and
-matches the real run's, so the same rounds are gated on.
+The coefficient fold is sharded (each rank folds its chunk of poly_k and
+the degree comes from the maxima of all ranks' chunks), and the loopback
+all-gather returns this rank's own maxima only, so the degree schedule of a
+1-GPU commit of the same polynomial is handed to the rehearsal
+(fri_debug_loopback_degrees): the same rounds are gated on as in the real run.
 
 The kernel trace then gives the rank's GPU time per commit, and the host
 clock the per-commit wall time with collectives that cost only a local copy.
@@ -38,13 +41,21 @@ def run(log_n, world, rank, steps, serial_coef=False):
     logw = world.bit_length() - 1
     d = (1 << log_n) >> 3
     coeffs = fo.splitmix64_np(42, d).astype("uint32")
+    one = fri_amd.Context(0, log_n)          # the degree schedule of the real commit
+    try:
+        one.commit(coeffs, log_n)
+        degrees = one.commit_degrees()
+    finally:
+        one.close()
     ctx = fri_amd.Context(0, log_n - logw)
     ctx.attach_loopback(rank, world)
+    ctx.loopback_degrees(degrees)
     if serial_coef:
         ctx.set_profiling(True)              # profiled commits run the coefficient folds on the main stream
     t0 = time.perf_counter()
     for _ in range(steps + 1):
         r = ctx.commit_sharded(coeffs, log_n)
+    assert r.n_layers == len(degrees), (r.n_layers, len(degrees))
     print(f"rank {rank}/{world}, 2^{log_n}: {r.n_layers} layers, {r.n_rounds} rounds; "
           f"{steps + 1} loopback commits in {time.perf_counter() - t0:.4f} s", flush=True)
     # timed as bench.py times the sharded step: coefficients resident in HBM
