@@ -805,6 +805,38 @@ def _cpu_baseline(coeffs, d, log_n):
     nthreads = lib.orc_num_threads()
     exp = _expected(log_n, 3)
     fast_ok = exp is not None and [bytes(r.roots[k]).hex() for k in range(r.n_layers)] == exp["roots"]
+    # Thread scaling of the same restatement at 2^20 (1 .. the allotted
+    # share), fitted with Amdahl's t(p) = s + w/p: the whole host's rate is
+    # that fit's extrapolation, labelled as such.  The GPU box allots each GPU
+    # a share of its host CPUs (OMP_NUM_THREADS, 16 per GPU) and asks jobs to
+    # stay within it, so nothing here runs on more threads than that.
+    L_s = min(log_n, 20)
+    cs20 = np.ascontiguousarray(fo.splitmix64_np(42, 1 << (L_s - 3)))
+    p20 = cs20.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+    def fast20():
+        ch = fo.OrcChannel()
+        lib.orc_channel_init(ctypes.byref(ch))
+        lib.orc_fri_commit_fast(p20, cs20.size, L_s, 5, 5, fo.P, ctypes.byref(ch), None, ctypes.byref(r), None, None)
+
+    scal = []
+    for th in sorted({1, 2, 4, 8, nthreads}):
+        if th > nthreads:
+            continue
+        lib.orc_set_num_threads(th)
+        scal.append((th, _median_runs(fast20, 3)[0]))
+    lib.orc_set_num_threads(nthreads)
+    As = np.array([[1.0, 1.0 / th] for th, _ in scal])
+    ys = np.array([t for _, t in scal])
+    (ser, par), *_ = np.linalg.lstsq(As / ys[:, None], np.ones_like(ys), rcond=None)
+    t_share = ser + par / nthreads
+    t_all = ser + par / max(1, host["nproc"] or 1)
+    all_cores = {"cores": host["nproc"], "extrapolated": True,
+                 "value": round((1 << log_n) / (t_fast * t_all / t_share), 1),
+                 "model": "Amdahl t(p) = s + w/p fitted to the 2^%d commit at p = %s threads; "
+                          "the 2^%d rate scaled by t(share)/t(nproc)" % (L_s, [th for th, _ in scal], log_n),
+                 "serial_fraction": round(float(ser / (ser + par)), 4),
+                 "measured_2p%d" % L_s: [{"threads": th, "seconds": round(t, 4)} for th, t in scal]}
     # faithful reference algorithm, single thread
     lib.orc_set_num_threads(1)
     pts = []
@@ -834,9 +866,11 @@ def _cpu_baseline(coeffs, d, log_n):
 
     return {"value": round((1 << log_n) / t_fast, 1), "unit": "field-elems/s", "cores": nthreads,
             "kind": "port", "host": host, "oracle_verified": fast_ok,
+            "cpu_share": {"threads": nthreads, "source": "OMP_NUM_THREADS (the GPU box's host-CPU share per GPU)"},
+            "all_cores": all_cores,
             "sample": f"full workload: OpenMP C restatement (NTT LDE, eval-form fold, SHA-256 Merkle, channel) "
-                      f"at codeword 2^{log_n}, median of 5 runs after 1 warm-up: {t_fast:.3f} s "
-                      f"(runs {', '.join(f'{t:.3f}' for t in runs)})",
+                      f"at codeword 2^{log_n} on the box's {nthreads}-thread CPU share, median of 5 runs after "
+                      f"1 warm-up: {t_fast:.3f} s (runs {', '.join(f'{t:.3f}' for t in runs)})",
             "faithful": {"kind": "port", "cores": 1,
                          "what": "reference algorithm (Horner LDE + coefficient fold + Horner re-evaluation, "
                                  "SHA-256 rs_merkle tree, hex channel), one thread",

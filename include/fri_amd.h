@@ -216,7 +216,14 @@ int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
  * next one's first with no host round trip in between.  A commit with another
  * (d, log_n, offset) first waits for the pending ones.  The read-backs
  * (fri_commit_info .. fri_decommit_query) serve the most recently enqueued
- * commit and wait for it.  Not while profiling (FRI_ESTATE). */
+ * commit and wait for it.  Not while profiling (FRI_ESTATE).
+ * d_coeffs is read when the commit runs on the device, not when the call
+ * returns: it must stay unchanged until fri_commit_wait(ticket) has returned.
+ * fri_ctx_input_buffer() is one buffer shared by every pending commit of the
+ * context, so refilling it while a commit is pending commits the new
+ * contents; give each pending commit its own device buffer, or use
+ * fri_commit_async, which copies host coefficients into the ticket's own
+ * pinned buffer before returning. */
 #define FRI_MAX_INFLIGHT 4
 int fri_commit_device_async(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t log_n,
                             uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,

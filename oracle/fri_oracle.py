@@ -561,9 +561,12 @@ def build_c_oracle() -> str:
 
 
 def load_c_oracle() -> ctypes.CDLL:
-    if not os.path.exists(ORACLE_SO):
+    # FRI_ORACLE_SO: another build of the same C oracle (tests/test_sanitizers.py
+    # loads the ASan/UBSan one, oracle/Makefile `asan`)
+    path = os.environ.get("FRI_ORACLE_SO", ORACLE_SO)
+    if path == ORACLE_SO and not os.path.exists(ORACLE_SO):
         build_c_oracle()
-    lib = ctypes.CDLL(ORACLE_SO)
+    lib = ctypes.CDLL(path)
     u64, sz, p64 = ctypes.c_uint64, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)
     for name in ("orc_fe_add", "orc_fe_sub", "orc_fe_mul", "orc_fe_pow", "orc_fe_div"):
         getattr(lib, name).restype = u64

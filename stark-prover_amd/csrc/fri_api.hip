@@ -159,6 +159,7 @@ struct fri_ctx {
     size_t trace_tree_cap = 0;      // leaves they can hold
     bool trace_valid = false;       // a trace commit is resident
     uint32_t trace_log_t = 0, trace_log_b = 0, trace_offset = 0;
+    bool stuck = false;               // a stream stayed busy after an RCCL abort (sync_sharded)
     bool inject_stall = false;        // fri_debug_inject_stall: next RCCL all-to-all never completes
     uint32_t* stall_flag = nullptr;   // pinned host word the stalled kernel polls (set by rccl_abort)
     uint32_t* stall_flag_dev = nullptr;
@@ -198,6 +199,14 @@ static void dfree(fri_ctx* ctx, const void* p) {
         }                                                                               \
     } while (0)
 
+static double rccl_timeout_s() {
+    const char* e = getenv("FRI_RCCL_TIMEOUT_S");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0.0 ? v : 120.0;
+}
+static double seconds_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
 static int fail(fri_ctx* ctx, int code, const std::string& msg) {
     if (ctx) ctx->err = msg;
     return code;
@@ -319,6 +328,21 @@ static void plan_free(fri_ctx* ctx) {
 extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     if (!ctx) return FRI_EINVAL;
     hipSetDevice(ctx->device);
+    if (ctx->stuck) {
+        // a stream that stayed busy after the RCCL abort: poll it with the
+        // deadline instead of an unbounded synchronize; if it is still busy,
+        // leak the context (its kernels may still touch its memory)
+        const auto t0 = std::chrono::steady_clock::now();
+        const double lim = rccl_timeout_s();
+        bool idle = false;
+        while (!(idle = (hipStreamQuery(ctx->stream) != hipErrorNotReady &&
+                         (!ctx->xstream || hipStreamQuery(ctx->xstream) != hipErrorNotReady) &&
+                         (!ctx->cstream || hipStreamQuery(ctx->cstream) != hipErrorNotReady))) &&
+               seconds_since(t0) < lim)
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        if (!idle) return FRI_ERCCL;
+        ctx->stuck = false;
+    }
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     // an upload whose commit was never enqueued (it failed) may still read
     // this context's pinned input buffers on the shared upload stream
@@ -957,9 +981,10 @@ static void settle(fri_ctx* ctx) {
 // Validate, build the plan and enqueue one commit on the context stream with
 // its DevState in `hs` (h_sync, or slot `slot` of the pipelined commits: each
 // slot replays its own graph, whose copy-out node targets that slot).
-static int commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
-                          uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
-                          const uint32_t* forced_betas, int slot) {
+// The argument checks of a 1-GPU commit (everything but the coefficients,
+// which the device validates): run before anything is copied or enqueued.
+static int commit_validate(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, uint32_t flags,
+                           const uint32_t* forced_betas) {
     if (log_n < 1 || log_n > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n out of range for context");
     const size_t n = (size_t)1 << log_n;
     if (d > n) return fail(ctx, FRI_EDEGREE, "more coefficients than domain points (domain would be exhausted)");
@@ -967,6 +992,14 @@ static int commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint3
     if ((flags & FRI_FLAG_FORCE_BETAS) && !forced_betas) return fail(ctx, FRI_EINVAL, "forced betas missing");
     if (forced_betas && (flags & FRI_FLAG_FORCE_BETAS) && !check_canonical(forced_betas, MAXR))
         return fail(ctx, FRI_EINVAL, "forced beta not canonical");
+    return FRI_OK;
+}
+
+static int commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
+                          uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                          const uint32_t* forced_betas, int slot) {
+    int rv = commit_validate(ctx, d, log_n, offset, flags, forced_betas);
+    if (rv) return rv;
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     int rc = plan_build(ctx, d, log_n, offset);     // a new plan waits for the pending commits (plan_free)
     if (rc) return rc;
@@ -1096,13 +1129,14 @@ static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32
         FRI_HIP(ctx, hipHostMalloc(&ctx->h_slot[slot], sizeof(DevState), hipHostMallocDefault));
         FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_slot[slot], hipEventDisableTiming));
     }
+    // every argument check before the pinned copy and the upload: a commit
+    // refused later would leave the slot free with its upload still in flight
+    int rv = commit_validate(ctx, d, log_n, offset, flags, forced_betas);
+    if (rv) return rv;
     if (host_coeffs && d) {
         // host input: pinned copy now, upload on h2d_stream (the copy engine,
         // beside the commit still running), the commit stream waits for it and
         // then moves it into the plan's input buffer (a device copy)
-        if (log_n >= 1 && log_n <= ctx->log_n_max && d > ((size_t)1 << log_n))
-            return fail(ctx, FRI_EDEGREE, "more coefficients than domain points (domain would be exhausted)");
-        if (d > ((size_t)1 << ctx->log_n_max)) return fail(ctx, FRI_EINVAL, "log_n out of range for context");
         if (!ctx->h2d_stream) FRI_HIP(ctx, upload_stream(ctx->device, &ctx->h2d_stream));
         if (!ctx->ev_in[slot]) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_in[slot], hipEventDisableTiming));
         if (ctx->h_in_cap[slot] < d) {       // the slot is free: its last upload and commit have completed
@@ -1122,7 +1156,12 @@ static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32
         d_coeffs = ctx->d_slot_in[slot];
     }
     int rc = commit_enqueue(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, slot);
-    if (rc) return rc;
+    if (rc) {
+        // the slot stays free: its upload must be over before the next call
+        // refills or frees the slot's buffers
+        if (host_coeffs && d) (void)hipEventSynchronize(ctx->ev_in[slot]);
+        return rc;
+    }
     FRI_HIP(ctx, hipEventRecord(ctx->ev_slot[slot], ctx->stream));
     ctx->slot_pending[slot] = true;
     ctx->slot_ticket[slot] = ctx->next_ticket++;
@@ -1498,14 +1537,6 @@ static int tp_host_stage(fri_ctx* ctx, size_t bytes) {
 // sharded path's stream syncs poll with it and abort the communicators (which
 // ends RCCL kernels spinning on an absent peer).  The sharded bench then
 // falls back to independent commits.
-static double rccl_timeout_s() {
-    const char* e = getenv("FRI_RCCL_TIMEOUT_S");
-    const double v = e ? atof(e) : 0.0;
-    return v > 0.0 ? v : 120.0;
-}
-static double seconds_since(std::chrono::steady_clock::time_point t0) {
-    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-}
 // Test hook (fri_debug_inject_stall): the next RCCL all-to-all is replaced by
 // a one-lane kernel that waits, like an RCCL kernel whose peer never comes,
 // until the abort releases it (or, as a bound every wave reaches, 60 s pass).
@@ -1560,6 +1591,7 @@ static int sync_sharded(fri_ctx* ctx, hipStream_t s) {
     bool drained = false;
     while (!(drained = hipStreamQuery(s) != hipErrorNotReady) && seconds_since(t1) < lim)
         std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (!drained) ctx->stuck = true;      // fri_ctx_destroy must not wait on it unboundedly
     return fail(ctx, FRI_ERCCL, "sharded commit: no progress in " + std::to_string((int)lim) +
                                     " s (RCCL communicators aborted" +
                                     (drained ? ")" : "; stream still busy: destroy the context)"));

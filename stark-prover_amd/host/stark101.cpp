@@ -332,29 +332,45 @@ std::vector<FRIProof> fri_commit_pipelined(const std::vector<Poly>& polys, uint3
         gpu->check(fri_commit_wait(gpu->ctx(), p.ticket, &res), "fri_commit_wait");
         out[p.i] = FRIProof::mirror(res, log_n, gpu, channels[p.i], p.gen);
     };
-    for (size_t i = 0; i < polys.size(); i++) {
-        if (pend.size() == 2) {
-            collect(pend.front());
+    try {
+        for (size_t i = 0; i < polys.size(); i++) {
+            if (pend.size() == 2) {
+                const Pending p = pend.front();
+                pend.erase(pend.begin());   // waited below even if collect throws
+                collect(p);
+            }
+            std::vector<uint32_t> coeffs = to_u32(polys[i].coefficients);
+            fri_channel_state cin{};
+            const fri_channel_state* pin = nullptr;
+            if (!channels[i].state.empty()) {
+                auto st = sha::from_hex(channels[i].state);
+                if (st.size() != 32) throw Panic("Channel state is not a SHA-256 digest");
+                std::memcpy(cin.digest, st.data(), 32);
+                cin.has_state = 1;
+                pin = &cin;
+            }
+            uint64_t ticket = 0;
+            const uint64_t gen = gpu->bump();          // this commit's layers replace the previous ones
+            gpu->check(fri_commit_async(gpu->ctx(), coeffs.data(), coeffs.size(), log_n,
+                                        static_cast<uint32_t>(offset.value()), pin, 0, nullptr, &ticket),
+                       "fri_commit_async");
+            pend.push_back({i, ticket, gen});
+        }
+        while (!pend.empty()) {
+            const Pending p = pend.front();
             pend.erase(pend.begin());
+            collect(p);
         }
-        std::vector<uint32_t> coeffs = to_u32(polys[i].coefficients);
-        fri_channel_state cin{};
-        const fri_channel_state* pin = nullptr;
-        if (!channels[i].state.empty()) {
-            auto st = sha::from_hex(channels[i].state);
-            if (st.size() != 32) throw Panic("Channel state is not a SHA-256 digest");
-            std::memcpy(cin.digest, st.data(), 32);
-            cin.has_state = 1;
-            pin = &cin;
+    } catch (...) {
+        // a failed commit (reported at its wait) must not leave the other
+        // result slots of this per-thread Gpu pending: wait for them all,
+        // discarding their results, then re-throw
+        for (const Pending& p : pend) {
+            fri_commit_result res{};
+            (void)fri_commit_wait(gpu->ctx(), p.ticket, &res);
         }
-        uint64_t ticket = 0;
-        const uint64_t gen = gpu->bump();          // this commit's layers replace the previous ones
-        gpu->check(fri_commit_async(gpu->ctx(), coeffs.data(), coeffs.size(), log_n,
-                                    static_cast<uint32_t>(offset.value()), pin, 0, nullptr, &ticket),
-                   "fri_commit_async");
-        pend.push_back({i, ticket, gen});
+        throw;
     }
-    for (const Pending& p : pend) collect(p);
     return out;
 }
 

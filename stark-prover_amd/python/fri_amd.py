@@ -948,6 +948,8 @@ def fri_commit_pipelined(polys: Sequence[Sequence[int]], log_n: int, channels: S
     if not 1 <= depth <= MAX_INFLIGHT:
         raise FriError(FRI_EINVAL, "depth must be 1..MAX_INFLIGHT")
     ctxs = list(ctx) if isinstance(ctx, (list, tuple)) else [ctx or _default_ctx(log_n)]
+    if len({id(c) for c in ctxs}) != len(ctxs):
+        raise FriError(FRI_EINVAL, "a context appears twice: pass each context once (depth sets the commits in flight)")
     gen = [c.commit_info()[0] for c in ctxs]     # every enqueued commit bumps its context's generation by one
     out: List[Optional[FRIProof]] = [None] * len(polys)
     pend = []
@@ -955,16 +957,26 @@ def fri_commit_pipelined(polys: Sequence[Sequence[int]], log_n: int, channels: S
     def collect(i, j, ticket, g):
         out[i] = _mirror_commit(ctxs[j].commit_wait(ticket), ctxs[j], log_n, channels[i], generation=g)
 
-    for i, (c, ch) in enumerate(zip(polys, channels)):
-        j = i % len(ctxs)
-        if len(pend) == depth * len(ctxs):
+    try:
+        for i, (c, ch) in enumerate(zip(polys, channels)):
+            j = i % len(ctxs)
+            if len(pend) == depth * len(ctxs):
+                collect(*pend.pop(0))
+            st = bytes.fromhex(ch.state) if ch.state else None
+            t = ctxs[j].commit_async(c, log_n, offset, channel_state=st)
+            gen[j] += 1
+            pend.append((i, j, t, gen[j]))
+        while pend:
             collect(*pend.pop(0))
-        st = bytes.fromhex(ch.state) if ch.state else None
-        t = ctxs[j].commit_async(c, log_n, offset, channel_state=st)
-        gen[j] += 1
-        pend.append((i, j, t, gen[j]))
-    for p in pend:
-        collect(*p)
+    finally:
+        # a commit that failed (e.g. a coefficient >= p, reported at its wait)
+        # must not leave the others' result slots pending on the contexts:
+        # wait for every remaining ticket, discarding its result
+        for _, j, t, _ in pend:
+            try:
+                ctxs[j].commit_wait(t)
+            except FriError:
+                pass
     return out
 
 
