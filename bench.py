@@ -197,20 +197,28 @@ def main():
             uid = torch.frombuffer(bytearray(fri_amd.Context.unique_id()), dtype=torch.uint8).clone()
         dist.broadcast(uid, 0)
 
-        def agreed(step):
+        def agreed(step, what):
             """Run one step of the sharded setup; every rank learns whether ALL
             ranks succeeded before anyone enters the next collective (a rank that
-            failed alone must not leave the others blocked inside RCCL)."""
+            failed alone must not leave the others blocked inside RCCL), and
+            which step failed on which ranks with what error (gloo all-gather),
+            so the fallback line names them on every rank."""
             nonlocal note
-            ok = 1
+            ok, msg = 1, None
             try:
                 if step() is False:
-                    ok, note = 0, note or "sharded transcript differed from the C oracle's"
+                    ok, msg = 0, "sharded transcript differed from the C oracle's"
             except fri_amd.FriError as e:
-                ok, note = 0, f"sharded path failed: {e}"
-            flag = torch.tensor([ok], dtype=torch.int32)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            return int(flag.item()) == 1
+                ok, msg = 0, str(e)
+            except Exception as e:  # noqa: BLE001 - any failure must reach the other ranks
+                ok, msg = 0, f"{type(e).__name__}: {e}"
+            every = [None] * world
+            dist.all_gather_object(every, (ok, msg))
+            bad = [r for r, (o, _) in enumerate(every) if not o]
+            if bad:
+                note = f"setup step '{what}' failed on rank(s) {bad}: {every[bad[0]][1]}"
+                print(f"[bench] rank {rank}: {note}", file=sys.stderr, flush=True)
+            return not bad
 
         attached = False
 
@@ -222,7 +230,8 @@ def main():
                 ctx.attach_rccl(rank, world, bytes(uid.numpy()))
             attached = True
 
-        ok = agreed(attach) and agreed(lambda: ctx.dist_selftest(4096))   # transport sanity first
+        ok = (agreed(attach, f"attach ({args.transport})")
+              and agreed(lambda: ctx.dist_selftest(4096), "transport self-test"))   # transport sanity first
         if ok:
             r_rank, r_world, r_kind = ctx.dist_info()
             dist_report = {"transport": r_kind, "world_reported": r_world, "rank_reported": r_rank}
@@ -239,7 +248,7 @@ def main():
                 ctypes.memmove(ctypes.byref(first), ctypes.byref(first_), ctypes.sizeof(first))
                 return True if exp is None else _matches(first_, exp)
 
-            if not agreed(first_commit):
+            if not agreed(first_commit, f"first sharded commit 2^{L} ({name})"):
                 if name.endswith("_primary"):
                     ok = False
                 else:
@@ -265,7 +274,7 @@ def main():
                                "value": round((1 << L) * k / el, 1), "unit": "field-elems/s", "steps": k,
                                "oracle_verified": exp is not None and _same(out, first) and _matches(out, exp)}
         if not ok:
-            fallback = note or "another rank failed during the sharded setup"
+            fallback = note or "the sharded setup failed"
             print(f"[bench] rank {rank}: {fallback}; falling back to replicas", file=sys.stderr, flush=True)
             if attached:
                 try:

@@ -87,7 +87,6 @@ struct DistBuf {
     uint32_t* cyc = nullptr;    // coset slice / all-to-all send
     uint32_t* recv = nullptr;   // all-to-all / gather receive
     uint32_t* half = nullptr;   // partner half-block
-    uint32_t* roots = nullptr;  // all-gathered block roots (rank order)
     uint32_t* top = nullptr;    // per-layer top trees (2G digests each)
     uint32_t* pre_lo = nullptr; // coset pre-scale tables
     uint32_t* pre_hi = nullptr;
@@ -95,10 +94,8 @@ struct DistBuf {
     uint32_t* gath = nullptr;   // all-gathered layer at the switch to local
     uint32_t* dq = nullptr;     // sharded decommitment: this rank's openings + all ranks' (G + 1 slots)
     uint32_t* rec = nullptr;    // per-layer record: this rank's (REC_WORDS) then all ranks' (64 * REC_WORDS)
-    int32_t* mx = nullptr;      // the G maxima triples of the current layer (k_tree_top's producers)
-    uint32_t* c0 = nullptr;     // poly_k coefficient 0 (the final value when deg_k = 0)
-    int32_t* sched = nullptr;   // loopback rehearsal: recorded degree per layer (fri_debug_loopback_degrees),
-    std::vector<int32_t> sched_h;   // uploaded by the next sharded commit
+    ShardTop* shtop = nullptr;  // per layer: what the sharded top kernels read (MAXR + 1)
+    std::vector<int32_t> sched_h;   // loopback rehearsal: recorded degree per layer (fri_debug_loopback_degrees)
 };
 
 // One timed launch group: events recorded around it on the context stream.
@@ -350,10 +347,9 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     plan_free(ctx);
     for (auto e : ctx->event_pool) hipEventDestroy(e);
     fri_dist_detach(ctx);
-    dfree(ctx, ctx->db.cyc); dfree(ctx, ctx->db.recv); dfree(ctx, ctx->db.half); dfree(ctx, ctx->db.roots);
+    dfree(ctx, ctx->db.cyc); dfree(ctx, ctx->db.recv); dfree(ctx, ctx->db.half);
     dfree(ctx, ctx->db.top); dfree(ctx, ctx->db.pre_lo); dfree(ctx, ctx->db.pre_hi); dfree(ctx, ctx->db.gath);
-    dfree(ctx, ctx->db.dq); dfree(ctx, ctx->db.rec); dfree(ctx, ctx->db.mx); dfree(ctx, ctx->db.c0);
-    dfree(ctx, ctx->db.sched);
+    dfree(ctx, ctx->db.dq); dfree(ctx, ctx->db.rec); dfree(ctx, ctx->db.shtop);
     if (ctx->xstream) hipStreamDestroy(ctx->xstream);
     if (ctx->ev_vals) hipEventDestroy(ctx->ev_vals);
     if (ctx->ev_xchg) hipEventDestroy(ctx->ev_xchg);
@@ -1612,9 +1608,10 @@ static void tp_log(fri_ctx* ctx, uint32_t chan, uint32_t op, int peer, size_t by
 static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
     Transport& tp = ctx->tp;
     tp_log(ctx, 0, FRI_OP_ALLGATHER, -1, bytes);
-    if (tp.loop) {
-        for (int r = 0; r < tp.world; r++)
-            FRI_HIP(ctx, hipMemcpyAsync((uint8_t*)drecv + (size_t)r * bytes, dsend, bytes, hipMemcpyDeviceToDevice, s));
+    if (tp.loop) {                     // G copies of this rank's bytes, one launch (bytes: whole words)
+        launch_replicate(static_cast<const uint32_t*>(dsend), static_cast<uint32_t*>(drecv), bytes / 4,
+                         (uint32_t)tp.world, s);
+        FRI_HIP(ctx, hipGetLastError());
         return FRI_OK;
     }
     if (!tp.host) {
@@ -1909,17 +1906,14 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
         FRI_HIP(ctx, dalloc(ctx, &b.half, (M / 2 + 1) * 4));
         b.cap = M;
     }
-    if (!b.roots) {
-        FRI_HIP(ctx, dalloc(ctx, &b.roots, 64 * 32));
+    if (!b.top) {
         FRI_HIP(ctx, dalloc(ctx, &b.top, (size_t)(MAXR + 1) * 2 * 64 * 32));
         FRI_HIP(ctx, dalloc(ctx, &b.pre_lo, ((size_t)1 << POW_LO_LOG) * 4));
         FRI_HIP(ctx, dalloc(ctx, &b.pre_hi, nhi * 4));
     }
     if (!b.rec) {
         FRI_HIP(ctx, dalloc(ctx, &b.rec, (size_t)(64 + 1) * REC_WORDS * 4));
-        FRI_HIP(ctx, dalloc(ctx, &b.mx, (size_t)64 * 3 * 4));
-        FRI_HIP(ctx, dalloc(ctx, &b.c0, 64));
-        FRI_HIP(ctx, dalloc(ctx, &b.sched, (size_t)(MAXR + 1) * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.shtop, (size_t)(MAXR + 1) * sizeof(ShardTop)));
     }
     if (b.gcap < gwords) {
         dfree(ctx, b.gath);
@@ -1940,10 +1934,6 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
     (void)G;
     return FRI_OK;
 }
-
-#ifndef SHARD_COEF_AFTER_LEAF
-#define SHARD_COEF_AFTER_LEAF 1
-#endif
 
 static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
                               uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
@@ -1974,11 +1964,6 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     if (rc) return rc;
     DistBuf& db = ctx->db;
     ctx->tp.log.clear();
-    if (ctx->tp.loop && !db.sched_h.empty()) {
-        std::vector<int32_t> sc(MAXR + 1, -1);
-        for (size_t i = 0; i < db.sched_h.size() && i <= (size_t)MAXR; i++) sc[i] = db.sched_h[i];
-        FRI_HIP(ctx, hipMemcpy(db.sched, sc.data(), sc.size() * 4, hipMemcpyHostToDevice));   // rehearsal only
-    }
     ctx->sharded_layers = (uint32_t)p.rmax + 1;      // lowered when the tail goes local
     init_state(ctx, ctx->h_sync, chan_in, flags, forced_betas);
     FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
@@ -2029,6 +2014,33 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         span_end(ctx, sp);
     }
 
+    // per-layer coefficient-task grid (workgroups over this rank's chunk S_k)
+    auto coef_grid = [&](int kk) {
+        const size_t S = (size_t)1 << (p.cs0 - (uint32_t)kk);
+        return (uint32_t)std::min<size_t>(2048, std::max<size_t>(1, (S + 8191) / 8192));
+    };
+    // what the sharded top kernels read per layer (ShardTop), for every layer
+    // this commit may run sharded: the block -> rank map follows the folds
+    {
+        std::vector<uint32_t> bo(G), ro(G);
+        for (uint32_t r = 0; r < G; r++) bo[r] = ro[r] = r;
+        std::vector<ShardTop> sh(MAXR + 1);
+        const bool sched = ctx->tp.loop && !db.sched_h.empty();
+        for (int kk = 0; kk <= p.k_sw && kk <= MAXR; kk++) {
+            ShardTop& t = sh[kk];
+            t.rec_out = db.rec;
+            t.rec_mx = p.wgmax;
+            t.rec_c0 = kk ? coef_buf(p, kk) : p.d_in;
+            t.rec_R = coef_grid(kk);
+            t.G = G;
+            t.recs_in = db.rec + REC_WORDS;
+            t.sched_on = sched ? 1u : 0u;
+            t.sched_deg = (sched && (size_t)kk < db.sched_h.size()) ? db.sched_h[kk] : -1;
+            for (uint32_t b2 = 0; b2 < G; b2++) t.rank_of_block[b2] = (uint8_t)ro[b2];
+            advance_blocks(bo, ro, G);
+        }
+        FRI_HIP(ctx, hipMemcpy(db.shtop, sh.data(), sh.size() * sizeof(ShardTop), hipMemcpyHostToDevice));
+    }
     std::vector<uint32_t> block_of(G), rank_of(G);
     for (uint32_t r = 0; r < G; r++) block_of[r] = rank_of[r] = r;
     int k = 0;
@@ -2083,44 +2095,34 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         tc.d0 = d;
         tc.wgmax = p.wgmax;
         tc.st = ctx->d_state;
-        uint32_t Gc = (uint32_t)((Sk + 8191) / 8192);
-        if (Gc < 1) Gc = 1;
-        if (Gc > 2048) Gc = 2048;
+        const uint32_t Gc = coef_grid(k);
         const bool side = !ctx->profiling;   // (profiled commits keep one stream for the spans)
-        // The fold starts when the block tree's leaf kernel has ended, beside
-        // its latency-bound mids and top: next to the VALU-bound leaf kernel it
-        // took 4x longer and slowed the leaves (tools/shard_projection.py)
-        if (side && !SHARD_COEF_AFTER_LEAF) {
-            FRI_HIP(ctx, hipEventRecord(ctx->ev_pre, s));
-            FRI_HIP(ctx, hipStreamWaitEvent(ctx->cstream, ctx->ev_pre, 0));
+        // The coefficient task starts when the block tree's leaf kernel has
+        // ended, beside its latency-bound mids: next to the VALU-bound leaf
+        // kernel it took 4x longer and slowed the leaves
+        // (tools/shard_projection.py).  The block top waits for it: it writes
+        // this rank's record (block root, the maxima of the coefficient
+        // slice, the slice's first coefficient) for the all-gather.
+        if (!side) launch_coef(tc, Gc, s);
+        auto coef_beside = [&]() {
+            (void)hipStreamWaitEvent(ctx->cstream, ctx->ev_pre, 0);
             launch_coef(tc, Gc, ctx->cstream);
-            FRI_HIP(ctx, hipEventRecord(ctx->ev_coef, ctx->cstream));
-        }
-        launch_layer(tl, s, side && SHARD_COEF_AFTER_LEAF ? ctx->ev_pre
-                                                          : spl == (size_t)-1 ? nullptr : ctx->spans[spl].e);
-        if (side && SHARD_COEF_AFTER_LEAF) {
-            FRI_HIP(ctx, hipStreamWaitEvent(ctx->cstream, ctx->ev_pre, 0));
-            launch_coef(tc, Gc, ctx->cstream);
-            FRI_HIP(ctx, hipEventRecord(ctx->ev_coef, ctx->cstream));
-        }
-        // this rank's record (block root, maxima of its coefficient slice, its
-        // first coefficient) -> all-gather -> top tree level 0 in block order,
-        // the G maxima triples and the final-value candidate of rank 0
-        if (side) FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_coef, 0));
-        else launch_coef(tc, Gc, s);
-        const int gate = k > 0 ? k - 1 : -1;
-        launch_shard_record(tl.tree + 8 * level_offset(tl.L, tl.L), p.wgmax, Gc, k ? tc.coef_out : p.d_in, db.rec,
-                            ctx->d_state, gate, s);
+            (void)hipEventRecord(ctx->ev_coef, ctx->cstream);
+        };
+        tl.shard = db.shtop + k;
+        launch_layer(tl, s, side ? ctx->ev_pre : (spl == (size_t)-1 ? nullptr : ctx->spans[spl].e),
+                     side ? std::function<void()>(coef_beside) : std::function<void()>(),
+                     side ? ctx->ev_coef : nullptr);
+        FRI_HIP(ctx, hipGetLastError());
+        // all ranks' records; the replicated top reads the block roots (in
+        // block order), the maxima and rank 0's first coefficient from them
         rc = tp_allgather(ctx, db.rec, db.rec + REC_WORDS, REC_WORDS * 4, s);
         if (rc) return rc;
-        uint32_t* top = db.top + (size_t)k * 2 * 64 * 8;
-        launch_shard_unpack(db.rec + REC_WORDS, G, block_of.data(), 0u, top, db.mx, db.c0,
-                            (ctx->tp.loop && !db.sched_h.empty()) ? db.sched : nullptr, k, ctx->d_state, gate, s);
         LayerTask tt = tc;
-        tt.tree = top;
+        tt.tree = db.top + (size_t)k * 2 * 64 * 8;
         tt.L = logG;
-        tt.coef_in = tt.coef_out = db.c0;    // k_tree_top's final value: poly_k[0] (rank 0's chunk)
-        launch_top(tt, 0, db.mx, G, s);
+        tt.shard = db.shtop + k;
+        launch_top(tt, 0, nullptr, G, s);
         span_end(ctx, spk);
         if (last) break;
         if (next_sharded) {
@@ -2158,9 +2160,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         // fixed by (G, rank)), so they replay as one hipGraph captured on the
         // first commit, without a launch gap per kernel
         auto local_tail = [&]() -> int {
-            for (uint32_t r = 0; r < G; r++)
-                FRI_HIP(ctx, hipMemcpyAsync(p.layers + p.layer_off[k] + (size_t)block_of[r] * B,
-                                            db.gath + (size_t)r * B, B * 4, hipMemcpyDeviceToDevice, s));
+            launch_place_blocks(db.gath, p.layers + p.layer_off[k], B, G, block_of.data(), s);
+            FRI_HIP(ctx, hipGetLastError());
             for (int kk = k + 1; kk <= p.rmax; kk++) {
                 if (log_n - (uint32_t)kk <= TAIL_LOG) {      // small layers: one launch
                     LayerTask ts[TAIL_LOG + 1];

@@ -8,7 +8,10 @@
 //                        rank's slice; block[G*t + r] = recv[r][t]
 //   pair fold           : layer k -> k+1 from the local half-block and the
 //                        partner's half-block (fri_commit.rs:53-65)
-//   root permute        : all-gathered block roots, rank order -> block order
+//   (the per-layer records of block roots and coefficient maxima are written
+//    and read by the sharded top kernels, k_tree_top<..., SHARD>, fri_layer.hip)
+#include <algorithm>
+
 #include "fri_internal.hpp"
 
 namespace fri {
@@ -95,79 +98,38 @@ void launch_radix2_block(const uint32_t* E, const uint32_t* O, const uint32_t* t
                        negate);
 }
 
-struct Perm64 { uint32_t p[64]; };
-// dst digest block_of_rank[r] <- src digest r  (G <= 64)
-__global__ void k_permute_digests(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t G, Perm64 pm) {
-    const uint32_t i = threadIdx.x;        // G * 8 words
-    if (i >= G * 8) return;
-    const uint32_t r = i / 8, w = i % 8;
-    dst[8 * pm.p[r] + w] = src[8 * r + w];
-}
-void launch_permute_digests(const uint32_t* src, uint32_t* dst, uint32_t G, const uint32_t* block_of_rank, hipStream_t s) {
-    Perm64 pm{};
-    for (uint32_t r = 0; r < G && r < 64; r++) pm.p[r] = block_of_rank[r];
-    hipLaunchKernelGGL(k_permute_digests, dim3(1), dim3(512), 0, s, src, dst, G, pm);
-}
-
-// Per-layer record of one rank (REC_WORDS words, all-gathered): its block
-// root, the maxima (m0, m1, m2) of its slice of the coefficient task
-// (reduced from the R workgroup triples) and its poly_k coefficient obase
-// (the final value when rank 0's chunk starts at 0 and deg_k == 0).
-// One wave; gated like the layer it belongs to.
-__global__ void k_shard_record(const uint32_t* __restrict__ root, const int32_t* __restrict__ wgmax, uint32_t R,
-                               const uint32_t* __restrict__ c0, uint32_t* __restrict__ rec, const DevState* st,
-                               int gate) {
-    if (gate >= 0 && !st->active[gate]) return;
-    const uint32_t t = threadIdx.x;
-    int a = -1, b = -1, c = -1;
-    for (uint32_t i = t; i < R; i += 64) {
-        a = max(a, wgmax[3 * i]); b = max(b, wgmax[3 * i + 1]); c = max(c, wgmax[3 * i + 2]);
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        a = max(a, __shfl_xor(a, off)); b = max(b, __shfl_xor(b, off)); c = max(c, __shfl_xor(c, off));
-    }
-    if (t < 8) rec[t] = root[t];
-    if (t == 0) {
-        rec[8] = (uint32_t)a; rec[9] = (uint32_t)b; rec[10] = (uint32_t)c;
-        rec[11] = c0 ? c0[0] : 0u;
-        rec[12] = rec[13] = rec[14] = rec[15] = 0u;
+// Switch to the local tail: the G gathered blocks (rank order) into their
+// places in the whole layer, block_of[r] * B, as one launch (16-byte copies).
+struct Blocks64 { uint32_t b[64]; };
+__global__ void k_place_blocks(const uint4* __restrict__ gath, uint4* __restrict__ layer, size_t B4, uint32_t G,
+                               Blocks64 bo) {
+    const size_t tot = B4 * G;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / B4, j = i - r * B4;
+        layer[(size_t)bo.b[r] * B4 + j] = gath[i];
     }
 }
-void launch_shard_record(const uint32_t* root, const int32_t* wgmax, uint32_t R, const uint32_t* c0, uint32_t* rec,
-                         const DevState* st, int gate, hipStream_t s) {
-    hipLaunchKernelGGL(k_shard_record, dim3(1), dim3(64), 0, s, root, wgmax, R, c0, rec, st, gate);
+void launch_place_blocks(const uint32_t* gath, uint32_t* layer, size_t B, uint32_t G, const uint32_t* block_of,
+                         hipStream_t s) {
+    Blocks64 bo{};
+    for (uint32_t r = 0; r < G && r < 64; r++) bo.b[r] = block_of[r];
+    const size_t tot = (B / 4) * G;
+    const unsigned blocks = (unsigned)std::min<size_t>(4096, (tot + 255) / 256);
+    hipLaunchKernelGGL(k_place_blocks, dim3(blocks ? blocks : 1), dim3(256), 0, s, reinterpret_cast<const uint4*>(gath),
+                       reinterpret_cast<uint4*>(layer), B / 4, G, bo);
 }
 
-// The G all-gathered records (rank order) -> the top tree's level 0 in block
-// order, the G maxima triples for k_tree_top (mx[3r..3r+2]) and the final
-// value candidate from the rank holding coefficient 0 (c0out).  sched
-// (loopback rehearsal only): the recorded degree of every layer replaces the
-// maxima, so one rank's share runs every round of the real commit.
-__global__ void k_shard_unpack(const uint32_t* __restrict__ recs, uint32_t G, Perm64 pm, uint32_t c0_rank,
-                               uint32_t* __restrict__ top, int32_t* __restrict__ mx, uint32_t* __restrict__ c0out,
-                               const int32_t* __restrict__ sched, int k, const DevState* st, int gate) {
-    if (gate >= 0 && !st->active[gate]) return;
-    const uint32_t i = threadIdx.x;
-    if (i < G * 8) {
-        const uint32_t r = i / 8, w = i % 8;
-        top[8 * pm.p[r] + w] = recs[REC_WORDS * r + w];
-    }
-    if (i < G * 3) {
-        const uint32_t r = i / 3, j = i % 3;
-        int32_t v = (int32_t)recs[REC_WORDS * r + 8 + j];
-        if (sched) v = j == 0 ? sched[k] : j == 1 ? (k == 0 ? -1 : 0) : -1;   // k = 0: deg = m0, canonical
-        mx[i] = v;
-    }
-    if (i == 0) c0out[0] = recs[REC_WORDS * c0_rank + 11];
+// Loopback rehearsal (fri_debug_attach_loopback): the all-gather of G
+// copies of this rank's bytes as one launch instead of G copies.
+__global__ void k_replicate(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, size_t words, uint32_t G) {
+    const size_t tot = words * G;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i % words];
 }
-void launch_shard_unpack(const uint32_t* recs, uint32_t G, const uint32_t* block_of_rank, uint32_t c0_rank,
-                         uint32_t* top, int32_t* mx, uint32_t* c0out, const int32_t* sched, int k, const DevState* st,
-                         int gate, hipStream_t s) {
-    Perm64 pm{};
-    for (uint32_t r = 0; r < G && r < 64; r++) pm.p[r] = block_of_rank[r];
-    hipLaunchKernelGGL(k_shard_unpack, dim3(1), dim3(512), 0, s, recs, G, pm, c0_rank, top, mx, c0out, sched, k, st,
-                       gate);
+void launch_replicate(const uint32_t* src, uint32_t* dst, size_t words, uint32_t G, hipStream_t s) {
+    const size_t tot = words * G;
+    const unsigned blocks = (unsigned)std::min<size_t>(2048, (tot + 255) / 256);
+    hipLaunchKernelGGL(k_replicate, dim3(blocks ? blocks : 1), dim3(256), 0, s, src, dst, words, G);
 }
 
 }  // namespace fri

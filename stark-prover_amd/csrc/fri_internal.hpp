@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <functional>
 #include "field.hpp"
 
 namespace fri {
@@ -111,6 +112,24 @@ void launch_decommit_gather(const uint32_t* layers, const uint32_t* trees, const
 void launch_fold_plain(const uint32_t* in, uint32_t* out, uint32_t log_m, const uint32_t* xinv_m,
                        uint32_t beta, hipStream_t s);
 
+// Sharded layer k (run_commit_sharded), device-resident per layer: what
+// the block top and the replicated top kernels of a coset-sharded layer read
+// besides their LayerTask (k_tree_top<..., SHARD>, fri_layer.hip).
+constexpr uint32_t REC_WORDS = 16;   // per-rank record: root (8), m0, m1, m2, first coefficient, 0 x 4
+struct ShardTop {
+    // block top (this rank): the record it writes
+    uint32_t* rec_out;
+    const int32_t* rec_mx;     // rec_R workgroup maxima triples of this rank's coefficient task
+    const uint32_t* rec_c0;    // this rank's first coefficient of poly_k
+    uint32_t rec_R;
+    // replicated top: the G all-gathered records (rank order)
+    uint32_t G;
+    const uint32_t* recs_in;
+    int32_t sched_deg;         // loopback rehearsal (sched_on): the recorded degree of this layer
+    uint32_t sched_on;
+    uint8_t rank_of_block[64]; // block b's root is in the record of rank rank_of_block[b]
+};
+
 // One FRI layer (fri_layer.hip): optional fold of the previous layer, leaf
 // hashes, every tree level, and (commit mode, st != nullptr) the coefficient
 // fold slice, degree resolution and Fiat-Shamir step of layer k.
@@ -134,8 +153,14 @@ struct LayerTask {
     // them); coef_in[0] holds global coefficient ibase of poly_{k-1} (of the
     // input at k == 0), coef_out[0] global coefficient obase of poly_k.
     size_t jlo, jhi, ibase, obase;
+    const ShardTop* shard;     // sharded layer (device): nullptr otherwise
 };
-void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end = nullptr);
+// after_leaf: called right after the leaf kernel is enqueued (and
+// ev_leaf_end recorded), so the caller can start work on another stream
+// behind it; ev_before_top: the stream waits for it before the top kernel
+// (a sharded block top reads the coefficient maxima made on that stream).
+void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end = nullptr,
+                  const std::function<void()>& after_leaf = {}, hipEvent_t ev_before_top = nullptr);
 // Layers ts[0..n) (consecutive, 2^L <= 2^TAIL_LOG elements, commit mode) in
 // one single-workgroup launch (k_tree_tail), n <= TAIL_LOG + 1.
 void launch_tail(const LayerTask* ts, uint32_t n, hipStream_t s);
@@ -150,18 +175,11 @@ void launch_radix2_block(const uint32_t* E, const uint32_t* O, const uint32_t* t
 void launch_cyclic_to_block(const uint32_t* recv, uint32_t* block, size_t B, uint32_t G, hipStream_t s);
 void launch_pair_fold(const uint32_t* first, const uint32_t* second, const uint32_t* xinv, uint32_t* out, size_t h,
                       const DevState* st, int r, hipStream_t s);
-void launch_permute_digests(const uint32_t* src, uint32_t* dst, uint32_t G, const uint32_t* block_of_rank,
-                            hipStream_t s);
-// Sharded coefficient fold: the per-layer record each rank all-gathers
-// (block root, maxima of its coefficient slice, its first coefficient) and
-// its unpacking on every rank (top level 0 in block order, G maxima triples,
-// the final-value candidate).
-constexpr uint32_t REC_WORDS = 16;
-void launch_shard_record(const uint32_t* root, const int32_t* wgmax, uint32_t R, const uint32_t* c0, uint32_t* rec,
-                         const DevState* st, int gate, hipStream_t s);
-void launch_shard_unpack(const uint32_t* recs, uint32_t G, const uint32_t* block_of_rank, uint32_t c0_rank,
-                         uint32_t* top, int32_t* mx, uint32_t* c0out, const int32_t* sched, int k, const DevState* st,
-                         int gate, hipStream_t s);
+// layer[block_of[r] * B ..] = gath[r * B ..] for r < G (B a multiple of 4).
+void launch_place_blocks(const uint32_t* gath, uint32_t* layer, size_t B, uint32_t G, const uint32_t* block_of,
+                         hipStream_t s);
+// Loopback rehearsal: dst = G copies of src (words each), one launch.
+void launch_replicate(const uint32_t* src, uint32_t* dst, size_t words, uint32_t G, hipStream_t s);
 // Tree top + degree + channel step for a layer whose level `l` (2^(L-l)
 // nodes, <= 512) is already in t.tree; mx/G: coefficient maxima.
 void launch_top(const LayerTask& t, uint32_t l, const int32_t* mx, uint32_t G, hipStream_t s);

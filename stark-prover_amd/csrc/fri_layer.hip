@@ -548,7 +548,16 @@ __device__ __forceinline__ uint32_t chan_beta(const uint32_t s[8]) {
 // at launch); wave 7 runs the channel jobs (chan_job) during the levels whose
 // nodes fit waves 0-2, then after the root, in extra iterations of the level
 // loop (uniform barrier count).
-template <bool FROM_LEAVES, bool FOLD, bool COMMIT>
+// SHARD (coset-sharded layers, run_commit_sharded; never FROM_LEAVES):
+//   !COMMIT: the top of this rank's block tree; it also writes the rank's
+//            per-layer record (t.shard->rec_out: block root, the maxima of
+//            its coefficient slice reduced from rec_R workgroup triples, its
+//            first coefficient), which the ranks then all-gather;
+//   COMMIT:  the replicated top of the layer: its N = G inputs are the block
+//            roots in the all-gathered records (rank order, permuted to block
+//            order and stored as the top tree's level 0), the maxima and the
+//            final-value candidate (rank 0's first coefficient) too.
+template <bool FROM_LEAVES, bool FOLD, bool COMMIT, bool SHARD = false>
 __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const int32_t* mx, uint32_t G) {
     if (gated_off(t)) return;
     __shared__ uint4 lds[2 * 1024 + 2 * 512];
@@ -601,12 +610,37 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
             }
         }
         if (COMMIT) coef_task(t, 0, 1, red);       // per-wave maxima in red[], wgmax[0..2]
+    } else if (SHARD && COMMIT) {
+        const ShardTop& sh = *t.shard;
+        for (uint32_t i = tid; i < N; i += blockDim.x) {
+            Dg d;
+            dg_load(sh.recs_in + REC_WORDS * sh.rank_of_block[i], d);
+            dg_lds_store(A + 2 * i, d);
+            dg_store(tr + 8 * i, d);               // level 0 of the top tree (decommitment paths)
+        }
+        int m0 = -1, m1 = -1, m2 = -1;
+        if (tid < sh.G) {
+            const int32_t* rm = reinterpret_cast<const int32_t*>(sh.recs_in + REC_WORDS * tid + 8);
+            m0 = rm[0]; m1 = rm[1]; m2 = rm[2];
+            if (sh.sched_on) { m0 = sh.sched_deg; m1 = t.k == 0 ? -1 : 0; m2 = -1; }   // loopback rehearsal
+        }
+        m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
+        if ((tid & 63) == 0) { red[3 * (tid >> 6)] = m0; red[3 * (tid >> 6) + 1] = m1; red[3 * (tid >> 6) + 2] = m2; }
     } else {
         const uint32_t* in = tr + 8 * level_offset(L, l);
         for (uint32_t i = tid; i < N; i += blockDim.x) {
             Dg d;
             dg_load(in + 8 * i, d);
             dg_lds_store(A + 2 * i, d);
+        }
+        if (SHARD && !COMMIT) {                    // this rank's coefficient-slice maxima
+            const ShardTop& sh = *t.shard;
+            int m0 = -1, m1 = -1, m2 = -1;
+            for (uint32_t i = tid; i < sh.rec_R; i += blockDim.x) {
+                m0 = max(m0, sh.rec_mx[3 * i]); m1 = max(m1, sh.rec_mx[3 * i + 1]); m2 = max(m2, sh.rec_mx[3 * i + 2]);
+            }
+            m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
+            if ((tid & 63) == 0) { red[3 * (tid >> 6)] = m0; red[3 * (tid >> 6) + 1] = m1; red[3 * (tid >> 6) + 2] = m2; }
         }
         if (COMMIT) {                              // producer maxima -> per-wave triples
             int m0 = -1, m1 = -1, m2 = -1;
@@ -631,7 +665,8 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     const bool is_final = COMMIT && deg < 1;
     const int job_end = is_final ? CJ_END_FINAL : CJ_END_ROUND;
     uint32_t fv = 0;                               // fri_commit.rs:109-113
-    if (chan_wave && is_final && deg == 0) fv = (t.k == 0 ? t.coef_in : t.coef_out)[0];
+    if (chan_wave && is_final && deg == 0)
+        fv = SHARD ? t.shard->recs_in[11] : (t.k == 0 ? t.coef_in : t.coef_out)[0];
     TOP_STAMP(1);
     TOP_CLK(17);
     // iterations: the levels, then the channel jobs still left after them
@@ -688,6 +723,18 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
             if (it < 11) TOP_STAMP(2 + it);
             if (it + 1 == nlev) { TOP_CLK(18); TOP_STAMP(19); }
         }
+    }
+    if (SHARD && !COMMIT && tid == 448) {          // this rank's record
+        const ShardTop& sh = *t.shard;
+        int m0 = -1, m1 = -1, m2 = -1;
+#pragma unroll
+        for (int i = 0; i < 8; i++) { m0 = max(m0, red[3 * i]); m1 = max(m1, red[3 * i + 1]); m2 = max(m2, red[3 * i + 2]); }
+        Dg root;
+        dg_lds_load(A, root);
+        uint32_t* rec = sh.rec_out;
+        dg_store(rec, root);
+        reinterpret_cast<uint4*>(rec)[2] = make_uint4((uint32_t)m0, (uint32_t)m1, (uint32_t)m2, sh.rec_c0[0]);
+        reinterpret_cast<uint4*>(rec)[3] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (!COMMIT || tid != 448) return;
     // ---- results (wave 7, one lane) ----
@@ -953,7 +1000,8 @@ static LayerTask with_gate(const LayerTask& in) {
 #define QUAD_MIN_LOG 19      // smaller layers: one leaf per lane (A/B: 19 beats 20 and 21)
 #endif
 
-void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
+void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end, const std::function<void()>& after_leaf,
+                  hipEvent_t ev_before_top) {
     const LayerTask t = with_gate(tin);
     const uint32_t L = t.L;
     const bool fold = t.prev != nullptr;
@@ -994,6 +1042,7 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
         }
     }
     if (ev_leaf_end) hipEventRecord(ev_leaf_end, s);
+    if (after_leaf) after_leaf();
     const int gate = t.gidx;
     // coefficient maxima: level 0 at wgmax[0 .. 3G); each mid reduces R producers per WG
     const int32_t* mx = commit ? t.wgmax : nullptr;
@@ -1019,7 +1068,9 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end) {
         out_per_wg = eight ? 1u : nin / 16;
         l += eight ? 8u : 4u;
     }
+    if (ev_before_top) hipStreamWaitEvent(s, ev_before_top, 0);
     if (commit) hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, mx, G);
+    else if (t.shard) hipLaunchKernelGGL((k_tree_top<false, false, false, true>), dim3(1), dim3(512), 0, s, t, l, nomx, G);
     else hipLaunchKernelGGL((k_tree_top<false, false, false>), dim3(1), dim3(512), 0, s, t, l, nomx, G);
 }
 
@@ -1045,7 +1096,8 @@ void launch_coef(const LayerTask& tin, uint32_t G, hipStream_t s) {
 
 void launch_top(const LayerTask& tin, uint32_t l, const int32_t* mx, uint32_t G, hipStream_t s) {
     const LayerTask t = with_gate(tin);
-    hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, mx, G);
+    if (t.shard) hipLaunchKernelGGL((k_tree_top<false, false, true, true>), dim3(1), dim3(512), 0, s, t, l, mx, G);
+    else hipLaunchKernelGGL((k_tree_top<false, false, true>), dim3(1), dim3(512), 0, s, t, l, mx, G);
 }
 
 }  // namespace fri
