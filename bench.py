@@ -79,6 +79,28 @@ def _same(a, b):
             and bytes(a.channel_out.digest) == bytes(b.channel_out.digest))
 
 
+def agree_step(dist, world, rank, step, what):
+    """Run one step of the sharded setup; every rank learns whether ALL ranks
+    succeeded before anyone enters the next collective (a rank that failed
+    alone must not leave the others blocked inside RCCL), and which step
+    failed on which ranks with what error (gloo all-gather), so the fallback
+    line names them on every rank.  Returns (ok, note)."""
+    ok, msg = 1, None
+    try:
+        if step() is False:
+            ok, msg = 0, "sharded transcript differed from the C oracle's"
+    except Exception as e:  # noqa: BLE001 - any failure (FriError or other) must reach the other ranks
+        ok, msg = 0, str(e) if type(e).__name__ == "FriError" else f"{type(e).__name__}: {e}"
+    every = [None] * world
+    dist.all_gather_object(every, (ok, msg))
+    bad = [r for r, (o, _) in enumerate(every) if not o]
+    if not bad:
+        return True, None
+    note = f"setup step '{what}' failed on rank(s) {bad}: {every[bad[0]][1]}"
+    print(f"[bench] rank {rank}: {note}", file=sys.stderr, flush=True)
+    return False, note
+
+
 def _expected(log_n, blowup_log):
     """Oracle transcript of the bench workload (tests/golden/bench_transcripts.json,
     written by tests/golden/make_bench_transcripts.py from the C oracle), or None."""
@@ -198,27 +220,11 @@ def main():
         dist.broadcast(uid, 0)
 
         def agreed(step, what):
-            """Run one step of the sharded setup; every rank learns whether ALL
-            ranks succeeded before anyone enters the next collective (a rank that
-            failed alone must not leave the others blocked inside RCCL), and
-            which step failed on which ranks with what error (gloo all-gather),
-            so the fallback line names them on every rank."""
             nonlocal note
-            ok, msg = 1, None
-            try:
-                if step() is False:
-                    ok, msg = 0, "sharded transcript differed from the C oracle's"
-            except fri_amd.FriError as e:
-                ok, msg = 0, str(e)
-            except Exception as e:  # noqa: BLE001 - any failure must reach the other ranks
-                ok, msg = 0, f"{type(e).__name__}: {e}"
-            every = [None] * world
-            dist.all_gather_object(every, (ok, msg))
-            bad = [r for r, (o, _) in enumerate(every) if not o]
-            if bad:
-                note = f"setup step '{what}' failed on rank(s) {bad}: {every[bad[0]][1]}"
-                print(f"[bench] rank {rank}: {note}", file=sys.stderr, flush=True)
-            return not bad
+            ok, msg = agree_step(dist, world, rank, step, what)
+            if not ok:
+                note = msg
+            return ok
 
         attached = False
 
@@ -560,9 +566,10 @@ def _decommit_stage(fri_amd, ctx, res, log_n, nq=64):
 def _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C, steps):
     import threading
     ctxs, ptrs, results = [ctx], [dptr], [fri_amd.CommitResult() for _ in range(C)]
+    seeds = [42 + (c % 3) for c in range(C)]          # distinct inputs: thread c commits seed 42 + c mod 3
     for c in range(1, C):
         cx = fri_amd.Context(ctx_device(ctx), log_n)
-        cx.commit(_coeffs(42, d, fri_amd.P), log_n)                  # same polynomial: same transcript
+        cx.commit(_coeffs(seeds[c], d, fri_amd.P), log_n)
         p = ctypes.c_void_p()
         cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p)))
         ctxs.append(cx)
@@ -582,39 +589,77 @@ def _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C, steps):
     for t in th:
         t.join()
     wall = time.perf_counter() - t0
-    ok = all(_same(r, res0) for r in results)
+    exps = [_expected_seed(log_n, sd) for sd in seeds]
+    ok = all(exps[c] is not None and _matches(r, exps[c]) for c, r in enumerate(results))
     for cx in ctxs[1:]:
         cx.close()
     return {"commits_in_flight": C, "ms_per_commit": round(1000.0 * wall / (C * steps), 4),
             "value": round(C * steps * (1 << log_n) / wall, 1), "unit": "field-elems/s", "transcripts_ok": ok,
-            "what": f"{C} host threads, one fri_ctx + stream each, {steps} commits of 2^{log_n} per thread"}
+            "what": f"{C} host threads, one fri_ctx + stream each, {steps} commits of 2^{log_n} per thread "
+                    "(thread c: seed 42 + c mod 3, transcripts checked against the C oracle's)"}
 
 
-def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps, depth=2):
-    """One context, one stream: commit k+1 is enqueued (fri_commit_device_async)
-    before commit k is collected (fri_commit_wait), so the device runs the
-    commits back to back without the host turnaround between them.  Every
-    collected transcript is compared with the first commit's."""
-    out = [fri_amd.CommitResult() for _ in range(steps)]
+def _expected_seed(log_n, seed):
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "bench_transcripts.json")) as f:
+            return json.load(f).get(f"{log_n}/{seed}/3")
+    except (OSError, ValueError):
+        return None
 
-    def run(k, results):
-        pend = []
-        for i in range(k):
-            pend.append(ctx.commit_device_async(dptr, d, log_n))
-            if len(pend) == depth:
-                ctx.commit_wait(pend.pop(0), results[i - depth + 1])
-        for j, t in enumerate(pend):
-            ctx.commit_wait(t, results[k - len(pend) + j])
 
-    run(depth, out)                                                  # warm-up: graphs of the slots
-    t0 = time.perf_counter()
-    run(steps, out)
-    wall = time.perf_counter() - t0
-    return {"depth": depth, "ms_per_commit": round(1000.0 * wall / steps, 4),
-            "value": round(steps * (1 << log_n) / wall, 1), "unit": "field-elems/s",
-            "transcripts_ok": all(_same(r, res0) for r in out),
-            "what": f"{steps} commits of 2^{log_n} on one fri_ctx, up to {depth} enqueued "
-                    "(fri_commit_device_async / fri_commit_wait): no host turnaround between commits"}
+def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps):
+    """ONE context, pipelined: up to `depth` commits pending
+    (fri_commit_device_async / fri_commit_wait), each on a commit lane of its
+    own (fri_ctx_set_lanes: a stream with its own plan), so one commit's
+    serial tree tops overlap the next commit's leaf hashing.  Distinct inputs:
+    three polynomials (splitmix64 seeds 42, 43, 44) in device buffers of their
+    own, dealt in turn; each buffer stays unchanged while its commits are
+    pending (fri_amd.h).  Every collected transcript is checked against the C
+    oracle's for its seed (tests/golden/bench_transcripts.json)."""
+    import numpy as np
+    import torch
+    seeds = (42, 43, 44)
+    exps = [_expected_seed(log_n, sd) for sd in seeds]
+    bufs = [torch.from_numpy(_coeffs(sd, d, fri_amd.P).view(np.int32)).to(f"cuda:{ctx_device(ctx)}") for sd in seeds]
+    ptrs = [ctypes.c_void_p(b.data_ptr()) for b in bufs]
+    torch.cuda.synchronize()
+    out = {}
+    for lanes, depth in ((1, 2), (2, 2), (3, 3), (4, 4)):
+        ctx.set_lanes(lanes)
+        res = [fri_amd.CommitResult() for _ in range(steps)]
+
+        def run(k):
+            pend = []
+            for i in range(k):
+                pend.append((i, ctx.commit_device_async(ptrs[i % 3], d, log_n)))
+                if len(pend) == depth:
+                    j, t = pend.pop(0)
+                    ctx.commit_wait(t, res[j % steps])
+            for j, t in pend:
+                ctx.commit_wait(t, res[j % steps])
+
+        run(2 * depth)                                              # warm-up: lane plans and slot graphs
+        t0 = time.perf_counter()
+        run(steps)
+        wall = time.perf_counter() - t0
+        ok = all(exps[i % 3] is not None and _matches(r, exps[i % 3]) for i, r in enumerate(res))
+        out[f"lanes_{lanes}"] = {"lanes": lanes, "depth": depth, "ms_per_commit": round(1000.0 * wall / steps, 4),
+                                 "value": round(steps * (1 << log_n) / wall, 1), "unit": "field-elems/s",
+                                 "transcripts_ok": ok}
+    ctx.set_lanes(fri_amd.MAX_INFLIGHT)
+    # lane 0's commits from the other buffers staged their inputs in the
+    # context's input buffer (dptr, fri_amd.h): put the seed-42 polynomial back
+    ctx._check(ctx.lib.fri_commit_device(ctx.h, ptrs[0], d, log_n, fri_amd.GENERATOR, None, 0, None,
+                                         ctypes.byref(fri_amd.CommitResult())))
+    best = min(out.values(), key=lambda v: v["ms_per_commit"])
+    out.update({"ms_per_commit": best["ms_per_commit"], "value": best["value"], "best_lanes": best["lanes"],
+                "transcripts_ok": all(v["transcripts_ok"] for v in out.values() if isinstance(v, dict)),
+                "hbm_bytes": ctx.device_bytes()[1],
+                "what": f"{steps} commits of 2^{log_n} on ONE fri_ctx, `depth` pending, dealt to `lanes` commit lanes "
+                        "(fri_commit_device_async / fri_commit_wait); 3 distinct polynomials (seeds 42-44), "
+                        "each transcript checked against the C oracle's"})
+    del bufs
+    return out
 
 
 def _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K, steps, depth=2):
@@ -622,9 +667,10 @@ def _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K, steps, depth=
     resident coefficients dealt round-robin with fri_commit_device_async, up
     to `depth` in flight per context, collected with fri_commit_wait."""
     ctxs, ptrs = [ctx], [dptr]
-    for _ in range(1, K):
+    seeds = [42 + (j % 3) for j in range(K)]          # distinct inputs: context j commits seed 42 + j mod 3
+    for j in range(1, K):
         cx = fri_amd.Context(ctx_device(ctx), log_n)
-        cx.commit(_coeffs(42, d, fri_amd.P), log_n)
+        cx.commit(_coeffs(seeds[j], d, fri_amd.P), log_n)
         p = ctypes.c_void_p()
         cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p)))
         ctxs.append(cx)
@@ -641,18 +687,23 @@ def _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K, steps, depth=
         for jj, t, k in pend:
             ctxs[jj].commit_wait(t, outs[k])
 
+    for cx in ctxs:
+        cx.set_lanes(1)                               # one stream per context: the concurrency is across contexts
     run(depth * K, [fri_amd.CommitResult() for _ in range(depth * K)])       # warm-up: slot graphs
     outs = [fri_amd.CommitResult() for _ in range(steps)]
     t0 = time.perf_counter()
     run(steps, outs)
     wall = time.perf_counter() - t0
-    ok = all(_same(r, res0) for r in outs)
+    exps = {sd: _expected_seed(log_n, sd) for sd in set(seeds)}
+    ok = all(exps[seeds[i % K]] is not None and _matches(r, exps[seeds[i % K]]) for i, r in enumerate(outs))
+    ctx.set_lanes(fri_amd.MAX_INFLIGHT)
     for cx in ctxs[1:]:
         cx.close()
     return {"contexts": K, "in_flight_per_context": depth, "ms_per_commit": round(1000.0 * wall / steps, 4),
             "value": round(steps * (1 << log_n) / wall, 1), "unit": "field-elems/s", "transcripts_ok": ok,
             "what": f"one host thread, {K} fri_ctx (one stream each), {steps} commits of 2^{log_n} dealt round-robin "
-                    "with fri_commit_device_async / fri_commit_wait"}
+                    "with fri_commit_device_async / fri_commit_wait; context j commits seed 42 + j mod 3, every "
+                    "transcript checked against the C oracle's"}
 
 
 def ctx_device(ctx):

@@ -202,7 +202,11 @@ int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t
                       const uint32_t* forced_betas, fri_commit_result* out);
 
 /* Device buffer of >= d words owned by the context that fri_commit_device
- * reads without a copy.  Valid until fri_ctx_destroy. */
+ * reads without a copy (commit lane 0's input buffer; synchronous commits run
+ * on lane 0).  Valid until the next commit with another (d, log_n, offset).
+ * A commit on lane 0 from any other device or host pointer copies its
+ * coefficients into this buffer; pipelined commits on other lanes copy from
+ * it into their own. */
 int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
 
 /* Pipelined commits: a prover that commits many codewords in a row calls
@@ -212,8 +216,8 @@ int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
  * ticket; fri_commit_wait(ticket) waits for that commit and returns its
  * result, with the same errors fri_commit_device would have returned.  Up to
  * FRI_MAX_INFLIGHT commits may be pending (FRI_ESTATE beyond that).  They run
- * one after another, so the device goes from one commit's last kernel to the
- * next one's first with no host round trip in between.  A commit with another
+ * on separate lanes (fri_ctx_set_lanes): concurrently, with no host round
+ * trip between one commit's kernels and the next one's.  A commit with another
  * (d, log_n, offset) first waits for the pending ones.  The read-backs
  * (fri_commit_info .. fri_decommit_query) serve the most recently enqueued
  * commit and wait for it.  Not while profiling (FRI_ESTATE).
@@ -235,6 +239,19 @@ int fri_commit_async(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32_t lo
                      uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                      const uint32_t* forced_betas, uint64_t* ticket);
 int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result* out);
+
+/* Commit lanes of pipelined commits.  Each lane is a stream with its own
+ * commit plan (input and coefficient buffers, layers, trees, x^-1 tables,
+ * graphs, device state); pending commit i goes to lane (result slot mod
+ * max_lanes), created on first use.  Commits on different lanes run
+ * concurrently, so one commit's serial tree tops (the Fiat-Shamir chain,
+ * one workgroup) overlap the next commit's leaf hashing on the otherwise
+ * idle chip.  Default FRI_MAX_INFLIGHT lanes: a caller keeping k commits
+ * pending uses k lanes and k plans of HBM (about 2.3 GB per 2^24 plan,
+ * 38 GB per 2^28 plan); max_lanes = 1 runs them one after another on one
+ * stream.  Lanes already created keep their memory until the next plan change
+ * or fri_ctx_destroy.  FRI_ESTATE while commits are pending. */
+int fri_ctx_set_lanes(fri_ctx* ctx, uint32_t max_lanes);
 
 /* Which commit the read-backs below serve: `generation` grows with every
  * commit call on the context (successful or not), log_n / n_layers describe

@@ -66,6 +66,20 @@ struct Plan {
     bool graph_profiled = false;
 };
 
+// One commit lane: a plan (every per-commit buffer: input, coefficient
+// buffers, layers, trees, x^-1 tables, graphs), the stream the lane's commits
+// run on and their device state.  Pipelined commits on one context are dealt
+// to lanes (result slot i -> lane i mod max_lanes, created on first use), so
+// consecutive commits run on different streams and one commit's serial tree
+// tops overlap the next one's leaf hashing.  The lane of the most recently
+// enqueued commit is the one installed in fri_ctx::{plan, stream, d_state}
+// (use_lane), so every read-back serves that commit.
+struct Lane {
+    Plan plan;
+    hipStream_t stream = nullptr;
+    DevState* d_state = nullptr;
+};
+
 // Collective transport of the sharded commit: RCCL on the context stream, or
 // host-staged callbacks (synchronous; used by the gloo tests).
 struct Transport {
@@ -133,6 +147,9 @@ struct fri_ctx {
     uint64_t next_ticket = 1;
     bool async_unsettled = false;   // commits enqueued since the stream was last drained
     Plan plan;
+    Lane lanes[FRI_MAX_INFLIGHT];   // lanes[cur_lane] is empty: that lane lives in plan / stream / d_state
+    int cur_lane = 0;
+    int max_lanes = FRI_MAX_INFLIGHT;
     bool profiling = false;
     std::map<std::string, ProfEntry> prof;
     std::vector<TimedSpan> spans;      // recorded spans of the current commit
@@ -306,9 +323,8 @@ extern "C" int fri_ctx_create(int device, uint32_t log_n_max, fri_ctx** out) {
 
 extern "C" int fri_dist_detach(fri_ctx* ctx);
 
-static void plan_free(fri_ctx* ctx) {
-    Plan& p = ctx->plan;
-    if (ctx->stream) hipStreamSynchronize(ctx->stream);   // pipelined commits may still use the plan
+// Free one plan's buffers and graphs (its lane's stream must be idle).
+static void plan_release(fri_ctx* ctx, Plan& p) {
     if (p.exec) hipGraphExecDestroy(p.exec);
     if (p.graph) hipGraphDestroy(p.graph);
     for (int i = 0; i < FRI_MAX_INFLIGHT; i++) {
@@ -320,6 +336,36 @@ static void plan_free(fri_ctx* ctx) {
     dfree(ctx, p.d_in); dfree(ctx, p.coefA); dfree(ctx, p.coefB); dfree(ctx, p.coefF); dfree(ctx, p.layers);
     dfree(ctx, p.trees); dfree(ctx, p.xinv); dfree(ctx, p.pre_lo); dfree(ctx, p.pre_hi); dfree(ctx, p.wgmax);
     p = Plan();
+}
+
+// Every lane's plan: pipelined commits may still use them, so every lane's
+// stream is drained first.
+static void plan_free(fri_ctx* ctx) {
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    for (Lane& ln : ctx->lanes)
+        if (ln.stream) hipStreamSynchronize(ln.stream);
+    plan_release(ctx, ctx->plan);
+    for (Lane& ln : ctx->lanes) plan_release(ctx, ln.plan);
+}
+
+// Install lane j in fri_ctx::{plan, stream, d_state} (creating its stream and
+// device state on first use); the lane installed before goes back to its slot.
+static int use_lane(fri_ctx* ctx, int j) {
+    if (j == ctx->cur_lane) return FRI_OK;
+    Lane& dst = ctx->lanes[j];
+    if (!dst.stream) {
+        FRI_HIP(ctx, hipStreamCreateWithFlags(&dst.stream, hipStreamNonBlocking));
+        if (dalloc(ctx, &dst.d_state, sizeof(DevState)) != hipSuccess) return fail(ctx, FRI_ENOMEM, "lane state");
+    }
+    Lane& park = ctx->lanes[ctx->cur_lane];
+    std::swap(park.plan, ctx->plan);
+    std::swap(park.stream, ctx->stream);
+    std::swap(park.d_state, ctx->d_state);
+    std::swap(dst.plan, ctx->plan);
+    std::swap(dst.stream, ctx->stream);
+    std::swap(dst.d_state, ctx->d_state);
+    ctx->cur_lane = j;
+    return FRI_OK;
 }
 
 extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
@@ -345,6 +391,11 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     // this context's pinned input buffers on the shared upload stream
     if (ctx->h2d_stream) hipStreamSynchronize(ctx->h2d_stream);
     plan_free(ctx);
+    for (Lane& ln : ctx->lanes) {
+        if (ln.stream) hipStreamDestroy(ln.stream);
+        dfree(ctx, ln.d_state);
+        ln = Lane();
+    }
     for (auto e : ctx->event_pool) hipEventDestroy(e);
     fri_dist_detach(ctx);
     dfree(ctx, ctx->db.cyc); dfree(ctx, ctx->db.recv); dfree(ctx, ctx->db.half);
@@ -804,10 +855,15 @@ static void plan_layout(Plan& p, size_t d, uint32_t log_n, uint32_t G, uint32_t 
 static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, uint32_t G = 1, uint32_t rank = 0) {
     Plan& p = ctx->plan;
     const bool sharded = G > 1;
-    if (p.valid && p.d == d && p.log_n == log_n && p.offset == offset && p.sharded == sharded && p.G == G &&
-        p.rank == rank)
-        return FRI_OK;
-    plan_free(ctx);
+    auto same = [&](const Plan& q) {
+        return q.d == d && q.log_n == log_n && q.offset == offset && q.sharded == sharded && q.G == G && q.rank == rank;
+    };
+    if (p.valid && same(p)) return FRI_OK;
+    // another shape: every lane's plan goes (after its pending commits); the
+    // same shape on other lanes: only this lane's plan is built
+    bool stale = p.valid;
+    for (const Lane& ln : ctx->lanes) stale = stale || (ln.plan.valid && !same(ln.plan));
+    if (stale) plan_free(ctx);
     const size_t n = (size_t)1 << log_n;
     size_t lay, tre, xin;
     plan_layout(p, d, log_n, G, rank, lay, tre, xin);
@@ -1067,7 +1123,11 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
                       uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                       const uint32_t* forced_betas, fri_commit_result* out) {
     if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
-    int rc = commit_enqueue(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, -1);
+    // synchronous commits run on lane 0, whose input buffer is the one
+    // fri_ctx_input_buffer hands out (after any commit pending on that lane)
+    int rc = use_lane(ctx, 0);
+    if (rc) return rc;
+    rc = commit_enqueue(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, -1);
     if (rc) return rc;
     FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
     ctx->async_unsettled = false;         // pending pipelined commits ran before this one
@@ -1121,14 +1181,17 @@ static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32
         if (!ctx->slot_pending[i]) slot = i;
     if (slot < 0) return fail(ctx, FRI_ESTATE, "FRI_MAX_INFLIGHT commits pending: wait for one first");
     FRI_HIP(ctx, hipSetDevice(ctx->device));
+    int rv = commit_validate(ctx, d, log_n, offset, flags, forced_betas);
+    if (rv) return rv;
+    // this commit's lane (its own stream, plan and device state): the
+    // commits pending on other lanes run beside it
+    if ((rv = use_lane(ctx, slot % ctx->max_lanes))) return rv;
     if (!ctx->h_slot[slot]) {
         FRI_HIP(ctx, hipHostMalloc(&ctx->h_slot[slot], sizeof(DevState), hipHostMallocDefault));
         FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_slot[slot], hipEventDisableTiming));
     }
-    // every argument check before the pinned copy and the upload: a commit
-    // refused later would leave the slot free with its upload still in flight
-    int rv = commit_validate(ctx, d, log_n, offset, flags, forced_betas);
-    if (rv) return rv;
+    // (every argument check ran before the pinned copy and the upload: a
+    // commit refused later would leave the slot free with its upload in flight)
     if (host_coeffs && d) {
         // host input: pinned copy now, upload on h2d_stream (the copy engine,
         // beside the commit still running), the commit stream waits for it and
@@ -1193,13 +1256,25 @@ extern "C" int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result*
     return commit_finish(ctx, ctx->h_slot[slot], ctx->slot_log_n[slot], out);
 }
 
+extern "C" int fri_ctx_set_lanes(fri_ctx* ctx, uint32_t max_lanes) {
+    if (!ctx) return FRI_EINVAL;
+    if (max_lanes < 1 || max_lanes > FRI_MAX_INFLIGHT) return fail(ctx, FRI_EINVAL, "lanes must be 1..FRI_MAX_INFLIGHT");
+    for (int i = 0; i < FRI_MAX_INFLIGHT; i++)
+        if (ctx->slot_pending[i]) return fail(ctx, FRI_ESTATE, "pipelined commits pending: wait for them first");
+    ctx->max_lanes = (int)max_lanes;
+    return FRI_OK;
+}
+
 extern "C" int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr) {
     if (!ctx || !d_ptr) return fail(ctx, FRI_EINVAL, "null argument");
     // The plan's input buffer is only stable for a fixed (d, log_n, offset);
     // the caller passes the returned pointer back to fri_commit_device, which
     // skips the copy when the pointers match.
-    if (!ctx->plan.valid || ctx->plan.d != d) return fail(ctx, FRI_ESTATE, "build a plan first (commit once with this d)");
-    *d_ptr = ctx->plan.d_in;
+    // lane 0's (synchronous commits run there; pipelined commits on other
+    // lanes copy from it into their own input buffers)
+    const Plan& p0 = ctx->cur_lane == 0 ? ctx->plan : ctx->lanes[0].plan;
+    if (!p0.valid || p0.d != d) return fail(ctx, FRI_ESTATE, "build a plan first (commit once with this d)");
+    *d_ptr = p0.d_in;
     return FRI_OK;
 }
 
@@ -1366,6 +1441,8 @@ extern "C" int fri_fibsq_composition_commit(fri_ctx* ctx, uint32_t log_t, uint32
         q.zinv_m[j] = to_mont(inv_std(z));
     }
     FRI_HIP(ctx, hipSetDevice(ctx->device));
+    int rl = use_lane(ctx, 0);            // the commit below runs on lane 0: so does its input
+    if (rl) return rl;
     hipStream_t s = ctx->stream;
     size_t sp = span_begin(ctx, "composition", (uint64_t)n * 8);
     launch_fibsq_cp(ctx->trace_lde, ctx->scratch_c, q, s);
@@ -1955,7 +2032,9 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     if (forced_betas && (flags & FRI_FLAG_FORCE_BETAS) && !check_canonical(forced_betas, MAXR))
         return fail(ctx, FRI_EINVAL, "forced beta not canonical");
     FRI_HIP(ctx, hipSetDevice(ctx->device));
-    int rc = plan_build(ctx, d, log_n, offset, G, rank);
+    int rc = use_lane(ctx, 0);            // sharded commits run on lane 0, like every synchronous commit
+    if (rc) return rc;
+    rc = plan_build(ctx, d, log_n, offset, G, rank);
     if (rc) return rc;
     Plan& p = ctx->plan;
     hipStream_t s = ctx->stream;

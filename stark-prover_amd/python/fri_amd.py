@@ -145,6 +145,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_decommit_query_sharded": (i32, [vp, ctypes.c_uint64, pu32, sz, ctypes.c_char_p, sz,
                                              ctypes.POINTER(sz)]),
         "fri_debug_loopback_degrees": (i32, [vp, ctypes.POINTER(ctypes.c_int32), u32]),
+        "fri_ctx_set_lanes": (i32, [vp, u32]),
         "fri_commit_degrees": (i32, [vp, ctypes.POINTER(ctypes.c_int32), sz, ctypes.POINTER(u32)]),
         "fri_debug_transport_log": (i32, [vp, ctypes.POINTER(TransportOp), sz, ctypes.POINTER(sz)]),
     }
@@ -300,6 +301,12 @@ class Context:
         self._check(self.lib.fri_commit_async(self.h, _ptr(c), c.size, log_n, offset, ctypes.byref(ch), 0, None,
                                               ctypes.byref(t)))
         return t.value
+
+    def set_lanes(self, max_lanes: int):
+        """Commit lanes of the pipelined commits (fri_ctx_set_lanes): pending
+        commit i runs on lane (slot mod max_lanes), each lane a stream with its
+        own plan, so consecutive commits overlap on the device."""
+        self._check(self.lib.fri_ctx_set_lanes(self.h, max_lanes))
 
     def commit_wait(self, ticket: int, out: Optional[CommitResult] = None) -> CommitResult:
         """Wait for an enqueued commit and return its result (fri_commit_wait)."""

@@ -299,3 +299,74 @@ def test_python_mirror_pipelined_over_contexts(oracle, oracle_commit):
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_commit_lanes(pctx, oracle, oracle_commit, torch):
+    """Commit lanes (fri_ctx_set_lanes): pending commit i runs on lane
+    (slot mod max_lanes), a stream with its own plan.  With 1..4 lanes every
+    transcript equals the oracle's; each lane in use holds one plan of HBM;
+    the limits of include/fri_amd.h hold."""
+    import fri_amd
+    d = (1 << LOG_N) >> 3
+    polys = _polys(oracle, torch, [1001, 1002, 1003, 1004, 1005, 1006])
+    want = {s: oracle_commit(LOG_N, s) for s, _ in polys}
+    pctx.commit(oracle.splitmix64_np(1001, d).astype(np.uint32), LOG_N)      # lane 0's plan
+    one_plan = pctx.device_bytes()[0]
+    for lanes in (1, 2, 3, 4):
+        pctx.set_lanes(lanes)
+        pend = []
+        for i, (s, buf) in enumerate(polys):
+            pend.append((s, pctx.commit_device_async(buf.data_ptr(), d, LOG_N)))
+            if len(pend) == lanes + 1 or len(pend) == fri_amd.MAX_INFLIGHT:
+                s0, t = pend.pop(0)
+                assert _transcript(pctx.commit_wait(t)) == want[s0], (lanes, s0)
+        for s0, t in pend:
+            assert _transcript(pctx.commit_wait(t)) == want[s0], (lanes, s0)
+        # read-backs serve the last commit, whichever lane it ran on
+        assert pctx.commit_info()[2] == LOG_N - 2
+        assert bytes(pctx.tree_level(0, LOG_N, LOG_N)[0]).hex() == want[polys[-1][0]]["roots"][0]
+    cur = pctx.device_bytes()[0]
+    assert cur > 3 * one_plan // 2, (cur, one_plan)          # several lanes' plans are resident
+    for bad in (0, fri_amd.MAX_INFLIGHT + 1):
+        with pytest.raises(fri_amd.FriError) as e:
+            pctx.set_lanes(bad)
+        assert e.value.code == fri_amd.FRI_EINVAL
+    t = pctx.commit_device_async(polys[0][1].data_ptr(), d, LOG_N)
+    with pytest.raises(fri_amd.FriError) as e:
+        pctx.set_lanes(2)                                    # commits pending
+    assert e.value.code == fri_amd.FRI_ESTATE
+    assert _transcript(pctx.commit_wait(t)) == want[polys[0][0]]
+
+
+def test_lanes_sync_commit_and_input_buffer(pctx, oracle, oracle_commit, torch):
+    """A synchronous commit runs on lane 0 while a pipelined commit is still
+    pending on lane 1; both transcripts are right and the read-backs then
+    serve the synchronous one.  The context's input buffer (lane 0's) stays
+    the same pointer across lanes, and a pipelined commit on another lane
+    reads it correctly."""
+    import fri_amd
+    d = (1 << LOG_N) >> 3
+    (s1, b1), (s2, b2) = _polys(oracle, torch, [1011, 1012])
+    c3 = oracle.splitmix64_np(1013, d).astype(np.uint32)
+    pctx.set_lanes(4)
+    pctx.commit(c3, LOG_N)
+    p0 = ctypes.c_void_p()
+    pctx._check(pctx.lib.fri_ctx_input_buffer(pctx.h, d, ctypes.byref(p0)))
+    t1 = pctx.commit_device_async(b1.data_ptr(), d, LOG_N)          # slot 0: lane 0
+    t2 = pctx.commit_device_async(b2.data_ptr(), d, LOG_N)          # slot 1: lane 1
+    assert _transcript(pctx.commit_wait(t1)) == oracle_commit(LOG_N, s1)
+    sync = pctx.commit(c3, LOG_N)                                    # lane 0, beside lane 1's pending commit
+    assert _transcript(sync) == oracle_commit(LOG_N, 1013)
+    assert _transcript(pctx.commit_wait(t2)) == oracle_commit(LOG_N, s2)
+    assert pctx.layer(2, LOG_N).size == 1 << (LOG_N - 2)
+    val, _ = pctx.auth_path(0, 5, LOG_N)
+    assert int(val) == int(pctx.lde(c3[:d], LOG_N)[5])               # the sync commit's layer 0
+    p1 = ctypes.c_void_p()
+    pctx._check(pctx.lib.fri_ctx_input_buffer(pctx.h, d, ctypes.byref(p1)))
+    assert p1.value == p0.value
+    ta = pctx.commit_device_async(b1.data_ptr(), d, LOG_N)          # lane 0 (stages b1 in the input buffer)
+    pctx.commit_wait(ta)
+    pctx.commit(c3, LOG_N)                                           # the input buffer holds c3 again
+    ts = [pctx.commit_device_async(p0.value, d, LOG_N) for _ in range(3)]   # lanes 0, 1, 2 read it
+    for t in ts:
+        assert _transcript(pctx.commit_wait(t)) == oracle_commit(LOG_N, 1013)
