@@ -386,18 +386,23 @@ def main():
 
     # (run before any stage that creates streams of its own: each context's
     # stream should get a hardware queue of its own, GPU_MAX_HW_QUEUES = 4)
+    # Queue sharing explains the round-3 gap between the bench and
+    # tools/multi_ctx_probe.py, see DESIGN.md §8.
     # Serving throughput: C independent commits in flight on one GPU (one
     # context + stream per host thread, the documented multi-context use).
     # The tree tops of one commit (one workgroup on the serial Fiat-Shamir
     # chain) overlap the leaf hashing of the others.  Beside `value`, never it.
+    # The multi-context stages run first (their contexts are destroyed after
+    # them), then the commit lanes of the one-context pipelined stage: every
+    # active stream then has a hardware queue of its own.
     concurrent = None
     pipelined = None
-    if world == 1 and mode == "single" and log_n >= 20:
-        pipelined = _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps=args.steps)
     if world == 1 and mode == "single" and log_n >= 20 and not args.no_extras:
         single = _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K=4, steps=max(12, args.steps))
         concurrent = _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C=3, steps=max(5, args.steps // 2))
         concurrent["single_thread_async"] = single
+    if world == 1 and mode == "single" and log_n >= 20:
+        pipelined = _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps=args.steps)
 
     # PCIe-inclusive rate (host coefficients in, result out): never `value`
     pcie = None
@@ -607,6 +612,26 @@ def _expected_seed(log_n, seed):
         return None
 
 
+def _hip_runtime():
+    """The HIP runtime libfri_amd.so is linked against (already loaded in
+    this process): device buffers for the bench's extra inputs without a
+    second runtime (PyTorch bundles its own libamdhip64)."""
+    path = "libamdhip64.so.7"
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64.so" in line and "/torch/" not in line:
+                    path = line.split()[-1]
+                    break
+    except OSError:
+        pass
+    hip = ctypes.CDLL(path)
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    return hip
+
+
 def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps):
     """ONE context, pipelined: up to `depth` commits pending
     (fri_commit_device_async / fri_commit_wait), each on a commit lane of its
@@ -616,13 +641,17 @@ def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps):
     own, dealt in turn; each buffer stays unchanged while its commits are
     pending (fri_amd.h).  Every collected transcript is checked against the C
     oracle's for its seed (tests/golden/bench_transcripts.json)."""
-    import numpy as np
-    import torch
     seeds = (42, 43, 44)
     exps = [_expected_seed(log_n, sd) for sd in seeds]
-    bufs = [torch.from_numpy(_coeffs(sd, d, fri_amd.P).view(np.int32)).to(f"cuda:{ctx_device(ctx)}") for sd in seeds]
-    ptrs = [ctypes.c_void_p(b.data_ptr()) for b in bufs]
-    torch.cuda.synchronize()
+    hip = _hip_runtime()
+    ptrs = []
+    for sd in seeds:
+        host = _coeffs(sd, d, fri_amd.P)
+        p = ctypes.c_void_p()
+        if hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(4 * d)) != 0 or \
+                hip.hipMemcpy(p, host.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(4 * d), 1) != 0:
+            return {"error": "hipMalloc / hipMemcpy of the input buffers failed"}
+        ptrs.append(p)
     out = {}
     for lanes, depth in ((1, 2), (2, 2), (3, 3), (4, 4)):
         ctx.set_lanes(lanes)
@@ -651,6 +680,8 @@ def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps):
     # context's input buffer (dptr, fri_amd.h): put the seed-42 polynomial back
     ctx._check(ctx.lib.fri_commit_device(ctx.h, ptrs[0], d, log_n, fri_amd.GENERATOR, None, 0, None,
                                          ctypes.byref(fri_amd.CommitResult())))
+    for p in ptrs:
+        hip.hipFree(p)
     best = min(out.values(), key=lambda v: v["ms_per_commit"])
     out.update({"ms_per_commit": best["ms_per_commit"], "value": best["value"], "best_lanes": best["lanes"],
                 "transcripts_ok": all(v["transcripts_ok"] for v in out.values() if isinstance(v, dict)),
@@ -658,7 +689,6 @@ def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps):
                 "what": f"{steps} commits of 2^{log_n} on ONE fri_ctx, `depth` pending, dealt to `lanes` commit lanes "
                         "(fri_commit_device_async / fri_commit_wait); 3 distinct polynomials (seeds 42-44), "
                         "each transcript checked against the C oracle's"})
-    del bufs
     return out
 
 
