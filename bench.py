@@ -629,6 +629,10 @@ def _hip_runtime():
     hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
     hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     hip.hipFree.argtypes = [ctypes.c_void_p]
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
     return hip
 
 
@@ -645,15 +649,29 @@ def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps):
     exps = [_expected_seed(log_n, sd) for sd in seeds]
     hip = _hip_runtime()
     ptrs = []
+    # the uploads go through a stream of their own that is destroyed again:
+    # a synchronous hipMemcpy would bring up the null stream, which keeps a
+    # hardware queue (GPU_MAX_HW_QUEUES = 4) and leaves one fewer for the lanes
+    st = ctypes.c_void_p()
+    via_null = os.environ.get("FRI_BENCH_NULL_STREAM_FILL") == "1"
+    if not via_null and hip.hipStreamCreate(ctypes.byref(st)) != 0:
+        return {"error": "hipStreamCreate failed"}
     for sd in seeds:
         host = _coeffs(sd, d, fri_amd.P)
         p = ctypes.c_void_p()
-        if hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(4 * d)) != 0 or \
-                hip.hipMemcpy(p, host.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(4 * d), 1) != 0:
-            return {"error": "hipMalloc / hipMemcpy of the input buffers failed"}
+        if hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(4 * d)) != 0:
+            return {"error": "hipMalloc of the input buffers failed"}
+        src = host.ctypes.data_as(ctypes.c_void_p)
+        rc = (hip.hipMemcpy(p, src, ctypes.c_size_t(4 * d), 1) if via_null else
+              hip.hipMemcpyAsync(p, src, ctypes.c_size_t(4 * d), 1, st) or hip.hipStreamSynchronize(st))
+        if rc != 0:
+            return {"error": "upload of the input buffers failed"}
         ptrs.append(p)
+    if not via_null:
+        hip.hipStreamDestroy(st)
     out = {}
-    for lanes, depth in ((1, 2), (2, 2), (3, 3), (4, 4)):
+    steps = max(steps, 60)
+    for lanes, depth in ((1, 2), (2, 2), (3, 3), (3, 4), (4, 4)):
         ctx.set_lanes(lanes)
         res = [fri_amd.CommitResult() for _ in range(steps)]
 
@@ -672,7 +690,7 @@ def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps):
         run(steps)
         wall = time.perf_counter() - t0
         ok = all(exps[i % 3] is not None and _matches(r, exps[i % 3]) for i, r in enumerate(res))
-        out[f"lanes_{lanes}"] = {"lanes": lanes, "depth": depth, "ms_per_commit": round(1000.0 * wall / steps, 4),
+        out[f"lanes_{lanes}_depth_{depth}"] = {"lanes": lanes, "depth": depth, "ms_per_commit": round(1000.0 * wall / steps, 4),
                                  "value": round(steps * (1 << log_n) / wall, 1), "unit": "field-elems/s",
                                  "transcripts_ok": ok}
     ctx.set_lanes(fri_amd.MAX_INFLIGHT)

@@ -1296,7 +1296,11 @@ extern "C" int fri_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out, size_
         return fail(ctx, FRI_ESTATE, "layer was committed sharded: this rank holds only its block (fri_commit_sharded)");
     size_t m = (size_t)1 << (p.log_n - layer);
     if (cap < m) return fail(ctx, FRI_EINVAL, "output buffer too small");
-    FRI_HIP(ctx, hipMemcpy(out, p.layers + p.layer_off[layer], m * 4, hipMemcpyDeviceToHost));
+    // on the context stream: the null stream would hold a hardware queue of
+    // its own (GPU_MAX_HW_QUEUES) for the rest of the process, one fewer for
+    // the commit lanes and other contexts
+    FRI_HIP(ctx, hipMemcpyAsync(out, p.layers + p.layer_off[layer], m * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return FRI_OK;
 }
 
@@ -1312,8 +1316,9 @@ extern "C" int fri_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level,
     size_t cnt = (size_t)1 << (L - level);
     if (cap < cnt * 32) return fail(ctx, FRI_EINVAL, "output buffer too small");
     std::vector<uint32_t> w(cnt * 8);
-    FRI_HIP(ctx, hipMemcpy(w.data(), p.trees + p.tree_off[layer] + 8 * level_offset(L, level), cnt * 32,
-                           hipMemcpyDeviceToHost));
+    FRI_HIP(ctx, hipMemcpyAsync(w.data(), p.trees + p.tree_off[layer] + 8 * level_offset(L, level), cnt * 32,
+                                hipMemcpyDeviceToHost, ctx->stream));   // (not the null stream: fri_layer_copy)
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
     for (size_t i = 0; i < cnt; i++) digest_to_bytes(&w[8 * i], out + 32 * i);
     return FRI_OK;
 }
@@ -2118,7 +2123,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
             for (uint32_t b2 = 0; b2 < G; b2++) t.rank_of_block[b2] = (uint8_t)ro[b2];
             advance_blocks(bo, ro, G);
         }
-        FRI_HIP(ctx, hipMemcpy(db.shtop, sh.data(), sh.size() * sizeof(ShardTop), hipMemcpyHostToDevice));
+        FRI_HIP(ctx, hipMemcpyAsync(db.shtop, sh.data(), sh.size() * sizeof(ShardTop), hipMemcpyHostToDevice, s));
+        FRI_HIP(ctx, hipStreamSynchronize(s));     // sh is a local: the copy completes here
     }
     std::vector<uint32_t> block_of(G), rank_of(G);
     for (uint32_t r = 0; r < G; r++) block_of[r] = rank_of[r] = r;
