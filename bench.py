@@ -693,7 +693,7 @@ def _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps):
         out[f"lanes_{lanes}_depth_{depth}"] = {"lanes": lanes, "depth": depth, "ms_per_commit": round(1000.0 * wall / steps, 4),
                                  "value": round(steps * (1 << log_n) / wall, 1), "unit": "field-elems/s",
                                  "transcripts_ok": ok}
-    ctx.set_lanes(fri_amd.MAX_INFLIGHT)
+    ctx.set_lanes(fri_amd.DEFAULT_LANES)
     # lane 0's commits from the other buffers staged their inputs in the
     # context's input buffer (dptr, fri_amd.h): put the seed-42 polynomial back
     ctx._check(ctx.lib.fri_commit_device(ctx.h, ptrs[0], d, log_n, fri_amd.GENERATOR, None, 0, None,
@@ -744,7 +744,7 @@ def _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K, steps, depth=
     wall = time.perf_counter() - t0
     exps = {sd: _expected_seed(log_n, sd) for sd in set(seeds)}
     ok = all(exps[seeds[i % K]] is not None and _matches(r, exps[seeds[i % K]]) for i, r in enumerate(outs))
-    ctx.set_lanes(fri_amd.MAX_INFLIGHT)
+    ctx.set_lanes(fri_amd.DEFAULT_LANES)
     for cx in ctxs[1:]:
         cx.close()
     return {"contexts": K, "in_flight_per_context": depth, "ms_per_commit": round(1000.0 * wall / steps, 4),

@@ -246,11 +246,17 @@ int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result* out);
  * max_lanes), created on first use.  Commits on different lanes run
  * concurrently, so one commit's serial tree tops (the Fiat-Shamir chain,
  * one workgroup) overlap the next commit's leaf hashing on the otherwise
- * idle chip.  Default FRI_MAX_INFLIGHT lanes: a caller keeping k commits
- * pending uses k lanes and k plans of HBM (about 2.3 GB per 2^24 plan,
- * 38 GB per 2^28 plan); max_lanes = 1 runs them one after another on one
- * stream.  Lanes already created keep their memory until the next plan change
- * or fri_ctx_destroy.  FRI_ESTATE while commits are pending. */
+ * idle chip.  Default FRI_DEFAULT_LANES (3) lanes: a caller keeping k <= 3
+ * commits pending uses k lanes and k plans of HBM (about 2.3 GB per 2^24
+ * plan, 38 GB per 2^28 plan); max_lanes = 1 runs them one after another on
+ * one stream.  Three, because HIP spreads a process's streams over its
+ * hardware queues (GPU_MAX_HW_QUEUES, 4 by default) in creation order: a
+ * fourth lane shared a queue with another and ran serialised with it
+ * (2^24: 3.41-3.45 ms per commit with 3 lanes and 3 pending, 3.75-3.86 with
+ * 4 and 4; profiles/r04_lanes_queues.txt).  Lanes already created keep their
+ * memory until the next plan change or fri_ctx_destroy.  FRI_ESTATE while
+ * commits are pending. */
+#define FRI_DEFAULT_LANES 3
 int fri_ctx_set_lanes(fri_ctx* ctx, uint32_t max_lanes);
 
 /* Which commit the read-backs below serve: `generation` grows with every

@@ -149,7 +149,7 @@ struct fri_ctx {
     Plan plan;
     Lane lanes[FRI_MAX_INFLIGHT];   // lanes[cur_lane] is empty: that lane lives in plan / stream / d_state
     int cur_lane = 0;
-    int max_lanes = FRI_MAX_INFLIGHT;
+    int max_lanes = FRI_DEFAULT_LANES;
     bool profiling = false;
     std::map<std::string, ProfEntry> prof;
     std::vector<TimedSpan> spans;      // recorded spans of the current commit

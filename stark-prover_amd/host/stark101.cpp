@@ -334,7 +334,7 @@ std::vector<FRIProof> fri_commit_pipelined(const std::vector<Poly>& polys, uint3
     };
     try {
         for (size_t i = 0; i < polys.size(); i++) {
-            if (pend.size() == 2) {
+            if (pend.size() == FRI_DEFAULT_LANES) {   // one pending commit per commit lane
                 const Pending p = pend.front();
                 pend.erase(pend.begin());   // waited below even if collect throws
                 collect(p);

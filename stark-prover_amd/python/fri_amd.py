@@ -38,6 +38,7 @@ FRI_OK, FRI_EINVAL, FRI_ENOMEM, FRI_EHIP, FRI_ENODEV, FRI_ERCCL, FRI_ESTATE, FRI
 FLAG_FORCE_BETAS = 1
 FLAG_NO_GRAPH = 2
 MAX_INFLIGHT = 4          # FRI_MAX_INFLIGHT (fri_amd.h): pipelined commits pending per context
+DEFAULT_LANES = 3         # FRI_DEFAULT_LANES (fri_amd.h): commit lanes of a context
 
 
 class FriError(RuntimeError):
@@ -942,11 +943,11 @@ def fri_commit(coeffs: Sequence[int], log_n: int, channel: Channel, offset: int 
 
 
 def fri_commit_pipelined(polys: Sequence[Sequence[int]], log_n: int, channels: Sequence[Channel],
-                         offset: int = GENERATOR, ctx=None, depth: int = 2) -> List[FRIProof]:
+                         offset: int = GENERATOR, ctx=None, depth: int = DEFAULT_LANES) -> List[FRIProof]:
     """fri_commit (fri_commit.rs:72-122) of many polynomials in a row, each
     with its own channel, pipelined from this one host thread
     (fri_commit_async / fri_commit_wait, ``depth`` commits in flight per
-    context).  ``ctx`` is one Context or a list of them: with several, the
+    context, each on a commit lane of its own: one context overlaps them).  ``ctx`` is one Context or a list of them: with several, the
     commits are dealt round-robin and run concurrently, one stream each.
     Proof i equals fri_commit of polys[i] into channels[i]; on each context
     only its last proof's layers stay resident."""
