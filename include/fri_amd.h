@@ -381,7 +381,9 @@ int fri_debug_stamps(fri_ctx* ctx, uint64_t* out, size_t cap);
 /* Host-only diagnostic (no context, no device): the commit plan's layout for
  * rank `rank` of `world` (world 1: the 1-GPU plan) of a codeword 2^log_n with
  * d coefficients.  out[0] = rounds bound R, out[1] = last sharded layer k_sw
- * (-1 for world 1), out[2] = bytes of layers + trees + x^-1 tables; then per
+ * (-1 for world 1), out[2] = bytes of layers + trees + x^-1 tables, out[3] =
+ * log2 of the coefficient chunk S_0 a rank folds (world > 1; rank r holds
+ * coefficients [r*S_k, (r+1)*S_k) of poly_k, S_k = S_0 / 2^k); then per
  * layer k <= R five words: layer-slot words, tree-slot words, x^-1 entries of
  * fold k, the domain index of the first of them, the block held of sharded
  * layer k.  cap >= 4 + 5 * FRI_MAX_LAYERS. */

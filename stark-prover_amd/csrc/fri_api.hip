@@ -1576,7 +1576,7 @@ extern "C" int fri_debug_plan_layout(size_t d, uint32_t log_n, uint32_t world, u
     out[0] = (uint64_t)p.rmax;
     out[1] = (uint64_t)(int64_t)p.k_sw;
     out[2] = 4 * (uint64_t)(lay + tre + xin);                 // bytes of layers + trees + x^-1 tables
-    out[3] = 0;
+    out[3] = p.cs0;                                            // sharded: log2 of the coefficient chunk S_0
     for (int k = 0; k <= p.rmax; k++) {
         uint64_t* o = out + 4 + 5 * (size_t)k;
         o[0] = p.layer_off[k + 1] - p.layer_off[k];            // words in layer slot k

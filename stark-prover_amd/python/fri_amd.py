@@ -578,7 +578,7 @@ def plan_layout(d: int, log_n: int, world: int = 1, rank: int = 0) -> dict:
                        (int(x) for x in out[4 + 5 * k: 9 + 5 * k]))) for k in range(rmax + 1)]
     k_sw = int(out[1])
     return {"rmax": rmax, "k_sw": k_sw - (1 << 64) if k_sw >= 1 << 63 else k_sw, "bytes": int(out[2]),
-            "layers": layers}
+            "coef_chunk_log2": int(out[3]), "layers": layers}
 
 
 # ----------------------------------------------------------------------------

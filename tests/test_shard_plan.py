@@ -93,3 +93,27 @@ def test_single_plan_layout():
         L = 24 - k
         assert lay["layer_words"] == 1 << L and lay["tree_words"] == 8 * ((2 << L) - 1)
         assert lay["xinv_count"] == ((1 << L) // 2 if k < 21 else 0)
+
+
+@pytest.mark.parametrize("G,log_n", list(itertools.product((2, 4, 8, 16, 64), (20, 22, 25, 28, 30))))
+@pytest.mark.parametrize("d_shape", ["n/8", "n", "odd", "tiny", "one", "zero"])
+def test_coefficient_chunks_cover_every_round(G, log_n, d_shape):
+    """The sharded coefficient fold (next_fri_polynomial, fri_commit.rs:32-50):
+    rank r folds coefficients [r*S_k, (r+1)*S_k) of poly_k with S_k = S_0/2^k.
+    The G chunks must cover every coefficient poly_k can have (ceil(d/2^k))
+    in every sharded round, each chunk must hold at least one coefficient
+    there (a pair c_2j, c_2j+1 of poly_{k-1} then never straddles two
+    chunks), and S_0 is the smallest power of two that does both."""
+    if log_n < (G.bit_length() - 1) + 12:
+        pytest.skip("codeword too small for this world")
+    n = 1 << log_n
+    d = {"n/8": n >> 3, "n": n, "odd": (n >> 3) + 12345, "tiny": 5, "one": 1, "zero": 0}[d_shape]
+    p = fri_amd.plan_layout(d, log_n, G, 0)
+    S0, k_sw = 1 << p["coef_chunk_log2"], p["k_sw"]
+    assert all(fri_amd.plan_layout(d, log_n, G, r)["coef_chunk_log2"] == p["coef_chunk_log2"] for r in (1, G - 1))
+    for k in range(0, k_sw + 1):
+        Sk = S0 >> k
+        assert Sk >= 1 and Sk << k == S0
+        assert G * Sk >= -(-d // (1 << k))            # every coefficient of poly_k has an owner
+    minimal = S0 == 1 or (G * (S0 // 2) < d) or (S0 // 2 < (1 << k_sw))
+    assert minimal, (S0, d, G, k_sw)
