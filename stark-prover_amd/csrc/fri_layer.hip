@@ -53,6 +53,18 @@ __device__ __forceinline__ uint32_t fold1(uint32_t a, uint32_t b, uint32_t xinv_
     return mmul(add(s, mmul(mmul(t, xinv_m), beta_m)), INV2_M2);
 }
 
+// Wave priority of the latency-bound chain kernels (tops, tail, narrow mids):
+// s_setprio raises their waves over co-resident throughput waves (another
+// commit lane's leaf hashing) in the SIMD's issue arbitration.  0 = off.
+// Three commit lanes: 3.50 -> 3.42 ms per 2^24 commit, synchronous commits
+// unchanged (3 interleaved rounds, profiles/r04_prio_*.txt).
+#ifndef FRI_CHAIN_PRIO
+#define FRI_CHAIN_PRIO 3
+#endif
+__device__ __forceinline__ void chain_prio() {
+    if (FRI_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(FRI_CHAIN_PRIO);
+}
+
 struct Dg { uint32_t w[8]; };
 
 __device__ __forceinline__ void dg_load(const uint32_t* p, Dg& d) {
@@ -299,6 +311,7 @@ __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
     lds_barrier();
     uint32_t cnt = 256;
     const shaq::Role qr = shaq::role_of(threadIdx.x);
+    if ((size_t)gridDim.x * 128 < WIDE_PAIR_MAX) chain_prio();   // from level 1 on, all on lane pairs
     const uint32_t nlev = wide_levels(L);
 #pragma unroll 1
     for (uint32_t j = 1; j <= nlev; j++) {
@@ -341,6 +354,7 @@ template <uint32_t NIN>
 __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st,
                                                       int gate, const int32_t* mx_in, int32_t* mx_out, uint32_t R) {
     if (st && gate >= 0 && !st->active[gate]) return;
+    if (NIN == 256) chain_prio();
     // level 1 reads its two inputs straight from HBM (64 contiguous bytes per
     // thread), so LDS holds only levels 1.. (NIN/2 + NIN/4 digests): more
     // workgroups per CU for the wide instance
@@ -394,6 +408,7 @@ __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L
 __global__ __launch_bounds__(256) void k_tree_mid8(uint32_t* tree, uint32_t L, uint32_t l, const DevState* st,
                                                    int gate, const int32_t* mx_in, int32_t* mx_out, uint32_t R) {
     if (st && gate >= 0 && !st->active[gate]) return;
+    chain_prio();
     __shared__ uint4 lds[256 + 128];
     uint4* A = lds;
     uint4* B = lds + 256;
@@ -560,6 +575,7 @@ __device__ __forceinline__ uint32_t chan_beta(const uint32_t s[8]) {
 template <bool FROM_LEAVES, bool FOLD, bool COMMIT, bool SHARD = false>
 __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const int32_t* mx, uint32_t G) {
     if (gated_off(t)) return;
+    chain_prio();
     __shared__ uint4 lds[2 * 1024 + 2 * 512];
     __shared__ int32_t red[24];
     const uint32_t L = t.L;
@@ -792,6 +808,7 @@ template <bool FOLD0>
 __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
     const LayerTask& t0 = tt.t[0];
     if (gated_off(t0)) return;
+    chain_prio();
     constexpr uint32_t NMAX = 1u << TAIL_LOG;
     __shared__ uint4 lds[2 * NMAX + NMAX];
     __shared__ uint32_t vals[2][NMAX];         // this / previous layer's values

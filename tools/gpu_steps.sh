@@ -18,6 +18,8 @@
 #   projkt  TAG [L]        kernel trace of one rank's share (rank 0 of 8) at 2^L (default 28),
 #                          summarised per kernel (tools/shard_projection.py)
 #   hiptrace TAG           HIP API + kernel trace around the commit graph (host turnaround)
+#   lanesab TAG A.so B.so  commit lanes (1 and 3 lanes) and synchronous commits, the two library
+#                          builds interleaved over 3 rounds (tools/lanes_probe.py, tools/abn.sh)
 set -e
 STEP=${1:?step}
 TAG=${2:?tag}
@@ -65,6 +67,14 @@ hiptrace)
         -d $O/${TAG}_hiptrace -o run -- \
         python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras --no-profile \
         > $O/${TAG}_hiptrace.json 2> $O/${TAG}_hiptrace.err
+    ;;
+lanesab)
+    for i in 1 2 3; do for lib in "$@"; do
+        echo "== $(basename $lib) round $i" >> $O/${TAG}_lanesab.txt
+        FRI_AMD_LIB=$lib timeout -k 10 120 python3 tools/lanes_probe.py --pairs 1:1,3:3 --commits 30 \
+            >> $O/${TAG}_lanesab.txt 2>&1
+    done; done
+    timeout -k 10 600 bash tools/abn.sh 3 20 "$@" > $O/${TAG}_syncab.txt 2>&1
     ;;
 *)
     echo "unknown step $STEP" >&2
