@@ -7,6 +7,10 @@ MODE "model": CPU model of the sharded commit (tests/dist_model.py) with the
               C oracle doing the per-block work and gloo doing the exchanges.
 MODE "gpu":   libfri_amd.so fri_commit_sharded on GPU 0 (every rank shares
               the one GPU), collectives staged through the host over gloo.
+MODE "gpu_fuzz": LOG_N random sharded commits (fuzz_case(SEED + i, W): ragged
+              coefficient counts, blowups 1..16, early-ending and zero
+              polynomials, random cosets, prefilled channels), one result per
+              case, plus each case's transport schedule.
 MODE "gpu_shard": the same on a context sized for one rank's shard only
               (log_n_max = log_n - log2 W; BASELINE configs[4] is 2^28 over
               8 ranks); reports the rank's HBM bytes, no 1-GPU re-commit.
@@ -49,6 +53,38 @@ def make_coeffs(kind, seed, d):
     return c
 
 
+def fuzz_case(i, world):
+    """Case i of the sharded fuzz (the same on every rank and in the test):
+    (log_n, coefficients as uint64, offset, prefilled channel state or None).
+    log_n >= 20 so that the commit really shards (SHARD_MIN_LOG)."""
+    import numpy as np
+    P = 3221225473
+    r = np.random.default_rng(50000 + i)
+    log_n = int(r.integers(20, 23))
+    n = 1 << log_n
+    kind = int(r.integers(0, 7))
+    if kind == 0:
+        d = n >> int(r.integers(0, 5))                 # blowup 1..16 (d > n/G: chunked coset reduction)
+    elif kind == 1:
+        d = int(r.integers(0, n + 1))                  # any count, 0 included
+    elif kind == 2:
+        d = int(r.integers(1, 65))                     # ends inside the sharded layers
+    else:
+        d = n >> 3
+    c = r.integers(0, P, size=d, dtype=np.uint64)
+    if d and kind == 3:
+        c[int(r.integers(0, d)):] = 0                  # trailing zeros: the degree from some rank's chunk
+    elif d and kind == 4:
+        c[:] = 0                                       # zero polynomial
+    elif d and kind == 5:
+        c[1:] = 0                                      # constant
+    elif d and kind == 6:
+        c[0::2] = 0                                    # add_assign's early return in round 1
+    offset = int(r.integers(1, P))
+    state = r.bytes(32) if r.integers(0, 2) else None
+    return log_n, c, offset, state
+
+
 def main():
     mode, log_n, seed, out_dir = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     blowup_log = int(sys.argv[5]) if len(sys.argv) > 5 else 3
@@ -59,6 +95,29 @@ def main():
     import numpy as np
 
     import fri_oracle as fo
+    if mode == "gpu_fuzz":
+        import fri_amd
+        ctx = fri_amd.Context(0, 22)
+        ctx.attach_torch(rank, world)
+        cases = []
+        for i in range(log_n):                         # LOG_N = number of cases
+            ln, c, offset, state = fuzz_case(seed + i, world)
+            try:
+                r = ctx.commit_sharded(c.astype(np.uint32), ln, offset, channel_state=state)
+            except fri_amd.FriError as e:
+                cases.append({"error": f"{e.code}: {e}"})
+                continue
+            cases.append({"roots": [bytes(r.roots[k]).hex() for k in range(r.n_layers)],
+                          "betas": [int(r.betas[j]) for j in range(r.n_rounds)],
+                          "final_value": int(r.final_value), "final_degree": int(r.final_degree),
+                          "state": bytes(r.channel_out.digest).hex(), "transport_log": ctx.transport_log()})
+        ctx.detach()
+        ctx.close()
+        with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+            json.dump({"cases": cases}, f)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     d = (1 << log_n) >> blowup_log
     coeffs = make_coeffs(kind, seed, d)
     if mode == "model":

@@ -144,6 +144,46 @@ def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, kind, corc,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,n_cases", [(2, 10), (4, 10), (8, 8)])
+def test_sharded_fuzz_vs_c_oracle(world, n_cases, corc, oracle):
+    """Randomised sharded commits (dist_worker.fuzz_case: 2^20..2^22, ragged
+    coefficient counts including 0, blowups 1..16, degrees that end the commit
+    inside the sharded layers, zero / constant / odd-only / trailing-zero
+    polynomials, random cosets, prefilled channels) on W ranks sharing GPU 0:
+    every root, beta, the final value and degree and the channel state equal
+    the OpenMP C oracle's 1-node commit (orc_fri_commit_fast, which follows
+    src/fri/fri_commit.rs:72-122), on every rank, and every case's transport
+    schedule passes the cross-rank check."""
+    import ctypes
+
+    import numpy as np
+    from dist_worker import fuzz_case
+    seed = 100 * world
+    got = run_ranks("gpu_fuzz", world, n_cases, seed, timeout=900)
+    for i in range(n_cases):
+        log_n, c, offset, state = fuzz_case(seed + i, world)
+        d = c.size
+        cs = np.ascontiguousarray(c, dtype=np.uint64)
+        och = oracle.OrcChannel()
+        corc.orc_channel_init(ctypes.byref(och))
+        if state is not None:
+            och.state = state.hex().encode()
+            och.state_len = 64
+        ores = oracle.OrcFriResult()
+        assert corc.orc_fri_commit_fast(cs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), d, log_n, offset, 5,
+                                        oracle.P, ctypes.byref(och), None, ctypes.byref(ores), None, None) == 0
+        what = f"case {seed + i}: world={world} log_n={log_n} d={d} offset={offset} prefilled={state is not None}"
+        want = {"roots": [bytes(ores.roots[k]).hex() for k in range(ores.n_layers)],
+                "betas": [ores.betas[j] for j in range(ores.n_rounds)],
+                "final_value": ores.final_value, "final_degree": ores.final_degree, "state": och.state.decode()}
+        for r in got:
+            case = r["cases"][i]
+            assert "error" not in case, (what, case)
+            assert {k: case[k] for k in want} == want, what
+        check_transport_schedule([r["cases"][i]["transport_log"] for r in got])
+
+
+@pytest.mark.gpu
 def test_loopback_rehearsal_transport(oracle):
     """fri_debug_attach_loopback (tools/shard_projection.py): one rank's share
     of a sharded commit runs on one device with every round of the real
