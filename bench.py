@@ -401,7 +401,7 @@ def main():
         single = _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K=4, steps=max(12, args.steps))
         concurrent = _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C=3, steps=max(5, args.steps // 2))
         concurrent["single_thread_async"] = single
-    if world == 1 and mode == "single" and log_n >= 20:
+    if world == 1 and mode == "single" and log_n >= 20 and not args.no_extras:
         pipelined = _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps=args.steps)
 
     # PCIe-inclusive rate (host coefficients in, result out): never `value`

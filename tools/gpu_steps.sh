@@ -41,8 +41,8 @@ parity)
     ;;
 collect)
     bash tools/collect_profiles.sh $TAG
-    bash tools/pmc_lde.sh 28 $O/prof_$TAG/pmc_lde_2p28.json
-    bash tools/pmc_lde.sh 24 $O/prof_$TAG/pmc_lde_2p24.json
+    bash tools/pmc_lde.sh 28 gpurun_out/prof_$TAG/pmc_lde_2p28.json
+    bash tools/pmc_lde.sh 24 gpurun_out/prof_$TAG/pmc_lde_2p24.json
     ;;
 proj)
     LS=${*:-28 24}
