@@ -205,8 +205,10 @@ int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t
  * reads without a copy (commit lane 0's input buffer; synchronous commits run
  * on lane 0).  Valid until the next commit with another (d, log_n, offset).
  * A commit on lane 0 from any other device or host pointer copies its
- * coefficients into this buffer; pipelined commits on other lanes copy from
- * it into their own. */
+ * coefficients into this buffer; a pipelined commit on another lane that is
+ * handed this buffer copies it into its own lane's buffer on lane 0's stream,
+ * so it reads the contents in call order (what the commits enqueued before it
+ * staged there, not what later ones stage). */
 int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
 
 /* Pipelined commits: a prover that commits many codewords in a row calls
@@ -224,8 +226,9 @@ int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
  * d_coeffs is read when the commit runs on the device, not when the call
  * returns: it must stay unchanged until fri_commit_wait(ticket) has returned.
  * fri_ctx_input_buffer() is one buffer shared by every pending commit of the
- * context, so refilling it while a commit is pending commits the new
- * contents; give each pending commit its own device buffer, or use
+ * context, so refilling it yourself while a commit that reads it is pending
+ * commits the new contents (the context's own stagings into it are ordered,
+ * see fri_ctx_input_buffer); give each pending commit its own device buffer, or use
  * fri_commit_async, which copies host coefficients into the ticket's own
  * pinned buffer before returning. */
 #define FRI_MAX_INFLIGHT 4

@@ -140,6 +140,9 @@ struct fri_ctx {
     uint64_t slot_ticket[FRI_MAX_INFLIGHT] = {};
     uint32_t slot_log_n[FRI_MAX_INFLIGHT] = {};
     bool slot_pending[FRI_MAX_INFLIGHT] = {};
+    // a pipelined commit on another lane handed lane 0's input buffer: its
+    // copy of that buffer, made on lane 0's stream, ends with this event
+    hipEvent_t ev_src[FRI_MAX_INFLIGHT] = {};
     uint32_t* h_in[FRI_MAX_INFLIGHT] = {};  // fri_commit_async: pinned copy of the slot's host coefficients,
     uint32_t* d_slot_in[FRI_MAX_INFLIGHT] = {};   // its device copy (uploaded on h2d_stream while the
     size_t h_in_cap[FRI_MAX_INFLIGHT] = {};       // previous commit runs) and the upload's event
@@ -421,6 +424,7 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     for (int i = 0; i < FRI_MAX_INFLIGHT; i++) {
         if (ctx->h_slot[i]) hipHostFree(ctx->h_slot[i]);
         if (ctx->ev_slot[i]) hipEventDestroy(ctx->ev_slot[i]);
+        if (ctx->ev_src[i]) hipEventDestroy(ctx->ev_src[i]);
         if (ctx->h_in[i]) hipHostFree(ctx->h_in[i]);
         dfree(ctx, ctx->d_slot_in[i]);
         if (ctx->ev_in[i]) hipEventDestroy(ctx->ev_in[i]);
@@ -1048,6 +1052,11 @@ static int commit_validate(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offs
     return FRI_OK;
 }
 
+// 0 only in a diagnostic build (tests/test_gpu_pipelined.py shows the race it closes)
+#ifndef FRI_LANE0_INPUT_ORDERED
+#define FRI_LANE0_INPUT_ORDERED 1
+#endif
+
 static int commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
                           uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                           const uint32_t* forced_betas, int slot) {
@@ -1062,10 +1071,24 @@ static int commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint3
     DevState* hs = slot < 0 ? ctx->h_sync : ctx->h_slot[slot];
     init_state(ctx, hs, chan_in, flags, forced_betas);
     ctx->commit_log_n = log_n;
-    if (host_coeffs && d)
+    const Lane& l0 = ctx->lanes[0];
+    if (FRI_LANE0_INPUT_ORDERED && slot >= 0 && ctx->cur_lane != 0 && d && dev_coeffs && l0.plan.valid &&
+        dev_coeffs == l0.plan.d_in) {
+        // Lane 0's input buffer (fri_ctx_input_buffer) handed to a commit on
+        // another lane.  Every commit on lane 0 from another pointer stages its
+        // coefficients into that buffer on lane 0's stream, so the copy is made
+        // there too: it reads what the buffer holds in call order (after the
+        // stagings of commits enqueued before this one, before those of later
+        // ones), and this lane's stream waits for it.
+        if (!ctx->ev_src[slot]) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_src[slot], hipEventDisableTiming));
+        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, l0.stream));
+        FRI_HIP(ctx, hipEventRecord(ctx->ev_src[slot], l0.stream));
+        FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_src[slot], 0));
+    } else if (host_coeffs && d) {
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
-    else if (dev_coeffs && dev_coeffs != p.d_in && d)
+    } else if (dev_coeffs && dev_coeffs != p.d_in && d) {
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, s));
+    }
     const bool use_graph = !(flags & FRI_FLAG_NO_GRAPH) && !ctx->profiling;
     if (use_graph) {
         // the DevState copies in (from the pinned state just written) and out

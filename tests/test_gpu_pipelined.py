@@ -370,3 +370,56 @@ def test_lanes_sync_commit_and_input_buffer(pctx, oracle, oracle_commit, torch):
     ts = [pctx.commit_device_async(p0.value, d, LOG_N) for _ in range(3)]   # lanes 0, 1, 2 read it
     for t in ts:
         assert _transcript(pctx.commit_wait(t)) == oracle_commit(LOG_N, 1013)
+
+
+def test_input_buffer_read_in_call_order_across_lanes(oracle, oracle_commit, torch):
+    """Lane 0's input buffer (fri_ctx_input_buffer) handed to a pipelined
+    commit D on lane 1: D must commit what the buffer holds in call order.
+    Commits on lane 0 from other pointers stage their coefficients into that
+    buffer, so D's copy of it is made on lane 0's stream (commit_enqueue in
+    fri_api.hip): after the stagings of the commits enqueued before D, before
+    those of later ones.  Here lane 0 runs two commits that stage a polynomial
+    with a coefficient >= p (they stop after layer 0 with FRI_EINVAL) while
+    lane 1 runs a whole 2^24 commit B before D; then a synchronous commit
+    stages P2.  In call order D reads the rejected polynomial, so D fails with
+    FRI_EINVAL; a copy made on lane 1's own stream would read P2 instead and
+    commit it.  A second round checks a valid staging: D then commits the
+    polynomial staged just before it."""
+    import fri_amd
+    L = 24
+    d = (1 << L) >> 3
+    cP, cQ, cP2, cP3 = (oracle.splitmix64_np(s, d).astype(np.uint32) for s in (2001, 2002, 2003, 2004))
+    bad = cQ.copy()
+    bad[d // 2] = fri_amd.P
+    dQ, dbad, dP3 = _dev(torch, cQ), _dev(torch, bad), _dev(torch, cP3)
+    cx = fri_amd.Context(0, L)
+    try:
+        cx.set_lanes(2)
+        cx.commit(cP, L)                                                # the input buffer holds P
+        p0 = ctypes.c_void_p()
+        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p0)))
+        tA = cx.commit_device_async(dbad.data_ptr(), d, L)              # slot 0: lane 0, stages bad, stops early
+        tB = cx.commit_device_async(dQ.data_ptr(), d, L)                # slot 1: lane 1, a whole commit
+        tC = cx.commit_device_async(dbad.data_ptr(), d, L)              # slot 2: lane 0, stages bad, stops early
+        tD = cx.commit_device_async(p0.value, d, L)                     # slot 3: lane 1, reads the buffer
+        for t in (tA, tC):
+            with pytest.raises(fri_amd.FriError) as e:
+                cx.commit_wait(t)
+            assert e.value.code == fri_amd.FRI_EINVAL
+        sync = cx.commit(cP2, L)                                        # lane 0: stages P2
+        with pytest.raises(fri_amd.FriError) as e:
+            cx.commit_wait(tD)
+        assert e.value.code == fri_amd.FRI_EINVAL, "D did not read the buffer in call order"
+        resB = _transcript(cx.commit_wait(tB))
+        # a valid staging just before D
+        tA = cx.commit_device_async(dP3.data_ptr(), d, L)               # slot 0: lane 0, stages P3
+        tB2 = cx.commit_device_async(dQ.data_ptr(), d, L)               # slot 1: lane 1
+        tD = cx.commit_device_async(p0.value, d, L)                     # slot 2: lane 0 (reads it directly)
+        tE = cx.commit_device_async(p0.value, d, L)                     # slot 3: lane 1, copy on lane 0's stream
+        cx.commit(cP2, L)                                               # stages P2 after all of them
+        res = [_transcript(cx.commit_wait(t)) for t in (tA, tB2, tD, tE)]
+    finally:
+        cx.close()
+    assert resB == oracle_commit(L, 2002)
+    assert _transcript(sync) == oracle_commit(L, 2003)
+    assert res == [oracle_commit(L, 2004), oracle_commit(L, 2002), oracle_commit(L, 2004), oracle_commit(L, 2004)]
