@@ -18,6 +18,8 @@
 #   projkt  TAG [L]        kernel trace of one rank's share (rank 0 of 8) at 2^L (default 28),
 #                          summarised per kernel (tools/shard_projection.py)
 #   hiptrace TAG           HIP API + kernel trace around the commit graph (host turnaround)
+#   final   TAG            end-of-round evidence in one call: suite (+ smoke), collect, proj,
+#                          and the 5000-shape commit fuzz
 #   lanesab TAG A.so B.so  commit lanes (1 and 3 lanes) and synchronous commits, the two library
 #                          builds interleaved over 3 rounds (tools/lanes_probe.py, tools/abn.sh)
 set -e
@@ -67,6 +69,13 @@ hiptrace)
         -d $O/${TAG}_hiptrace -o run -- \
         python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras --no-profile \
         > $O/${TAG}_hiptrace.json 2> $O/${TAG}_hiptrace.err
+    ;;
+final)
+    bash tools/gpu_steps.sh suite $TAG
+    bash tools/gpu_steps.sh collect $TAG
+    bash tools/gpu_steps.sh proj $TAG
+    FRI_FUZZ_N=5000 timeout -k 10 600 python -u -m pytest tests/test_gpu_fuzz.py -q -m gpu --timeout 500 \
+        --timeout-method thread > $O/${TAG}_fuzz5000.log 2>&1
     ;;
 lanesab)
     for i in 1 2 3; do for lib in "$@"; do
