@@ -1080,7 +1080,13 @@ static int commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint3
         // there too: it reads what the buffer holds in call order (after the
         // stagings of commits enqueued before this one, before those of later
         // ones), and this lane's stream waits for it.
+        // The copy overwrites this lane's own input buffer, which the commits
+        // already queued on this lane may still read: lane 0's stream first
+        // waits for them (the event is re-recorded after the copy; each wait
+        // binds to the record before it).
         if (!ctx->ev_src[slot]) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_src[slot], hipEventDisableTiming));
+        FRI_HIP(ctx, hipEventRecord(ctx->ev_src[slot], s));
+        FRI_HIP(ctx, hipStreamWaitEvent(l0.stream, ctx->ev_src[slot], 0));
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, l0.stream));
         FRI_HIP(ctx, hipEventRecord(ctx->ev_src[slot], l0.stream));
         FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_src[slot], 0));
