@@ -42,11 +42,11 @@ def transcript(r):
             bytes(r.channel_out.digest).hex())
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--commits", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=1)
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     import torch
     import fri_amd
     import fri_oracle as fo
@@ -140,6 +140,7 @@ def main():
     print(f"soak ok: {n_ok} commits checked against the C oracle in {time.time() - t0:.1f} s "
           f"(kinds: sync-host {kinds.get(0, 0)}, sync-device {kinds.get(1, 0)}, async-device {kinds.get(2, 0)}, "
           f"async-host {kinds.get(3, 0)}, async-input-buffer {kinds.get(4, 0)})", flush=True)
+    return n_ok, kinds
 
 
 if __name__ == "__main__":
