@@ -14,11 +14,13 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("seed", [11, 12])
-def test_soak_mixed_entry_points(seed):
+@pytest.mark.parametrize("seed,contexts", [(11, 1), (12, 1), (13, 3)])
+def test_soak_mixed_entry_points(seed, contexts):
+    """One context, and three contexts driven round-robin at random from one
+    thread (their host-input uploads share the device's upload stream)."""
     spec = importlib.util.spec_from_file_location("soak", os.path.join(ROOT, "tools", "soak.py"))
     soak = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(soak)
-    n_ok, kinds = soak.main(["--commits", "3000", "--seed", str(seed)])
+    n_ok, kinds = soak.main(["--commits", "3000", "--seed", str(seed), "--contexts", str(contexts)])
     assert n_ok == 3000
     assert all(kinds.get(k, 0) > 200 for k in range(5)), kinds

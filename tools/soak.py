@@ -1,17 +1,19 @@
-"""Soak test of one context under a random mix of commit entry points (GPU).
+"""Soak test of commit contexts under a random mix of entry points (GPU).
 
-Thousands of commits on ONE fri_ctx, drawn at random from: synchronous
-commits from host coefficients or from a device buffer, pipelined commits of
-device buffers, of host coefficients (fri_commit_async) and of the context's
-own input buffer (fri_ctx_input_buffer), with the number of commit lanes and
-the codeword shape changing now and then.  Every result is compared with the
-C oracle's transcript of the same polynomial (oracle/fri_oracle.c, the
-restatement of src/fri/fri_commit.rs:72-122), so an ordering race between
-lanes, stagings or slots shows up as a wrong transcript.  The input buffer's
-expected contents follow call order: a commit handed that buffer commits what
-the last synchronous commit or lane-0 staging put there.
+Thousands of commits on one or more fri_ctx driven from ONE host thread,
+each drawn at random from: synchronous commits from host coefficients or from
+a device buffer, pipelined commits of device buffers, of host coefficients
+(fri_commit_async; every context's uploads share the device's upload stream)
+and of the context's own input buffer (fri_ctx_input_buffer), with the number
+of commit lanes and the codeword shape of a context changing now and then.
+Every result is compared with the C oracle's transcript of the same
+polynomial (oracle/fri_oracle.c, the restatement of
+src/fri/fri_commit.rs:72-122), so an ordering race between lanes, stagings,
+result slots or contexts shows up as a wrong transcript.  A context's input
+buffer follows call order: a commit handed that buffer commits what the last
+synchronous commit or lane-0 staging of that context put there.
 
-    python3 tools/soak.py [--commits N] [--seed S]
+    python3 tools/soak.py [--commits N] [--seed S] [--contexts K]
 """
 import argparse
 import ctypes
@@ -24,6 +26,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "stark-prover_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+SHAPES = [16, 18, 20]                              # log_n; d = n / 8
 
 
 def oracle_transcript(corc, fo, c, log_n):
@@ -42,102 +46,113 @@ def transcript(r):
             bytes(r.channel_out.digest).hex())
 
 
+class Driven:
+    """One context and the model of its state: the result slot of every
+    pending ticket (lowest free slot, fri_api.hip async_enqueue), its lanes,
+    its shape and what its input buffer holds in call order."""
+
+    def __init__(self, fri_amd, polys, rng):
+        self.fa, self.polys, self.rng = fri_amd, polys, rng
+        self.ctx = fri_amd.Context(0, max(SHAPES))
+        self.lanes = 3
+        self.ctx.set_lanes(self.lanes)
+        self.slots, self.pend = {}, []
+        self.L = SHAPES[0]
+        self.in_buf = None
+        self.n_ok = 0
+
+    def next_lane(self):
+        return min(set(range(self.fa.MAX_INFLIGHT)) - set(self.slots.values())) % self.lanes
+
+    def enqueue(self, t, key):
+        self.slots[t] = min(set(range(self.fa.MAX_INFLIGHT)) - set(self.slots.values()))
+        self.pend.append((t, key))
+
+    def expect_oldest(self):
+        t, key = self.pend.pop(0)
+        self.slots.pop(t)
+        r = self.ctx.commit_wait(t)
+        assert transcript(r) == self.polys[key][2], f"pipelined commit of {key} gave a wrong transcript"
+        self.n_ok += 1
+
+    def drain(self):
+        while self.pend:
+            self.expect_oldest()
+
+    def step(self, kinds):
+        fa, rng, ctx = self.fa, self.rng, self.ctx
+        u = rng.random()
+        if u < 0.02:                               # another shape: every lane's plan is rebuilt
+            self.drain()
+            self.L = int(rng.choice(SHAPES))
+            self.in_buf = None
+        elif u < 0.04:                             # another number of lanes (no commit may be pending)
+            self.drain()
+            self.lanes = int(rng.integers(1, fa.MAX_INFLIGHT + 1))
+            ctx.set_lanes(self.lanes)
+        L = self.L
+        d = (1 << L) >> 3
+        j = int(rng.integers(0, 4))
+        kind = int(rng.integers(0, 5))
+        if kind == 4 and self.in_buf is None:
+            kind = 0
+        if len(self.pend) == fa.MAX_INFLIGHT:
+            self.expect_oldest()
+        c, dev, want = self.polys[(L, j)]
+        if kind == 0:                              # synchronous, host coefficients: staged (lane 0)
+            assert transcript(ctx.commit(c, L)) == want
+            self.n_ok += 1
+            self.in_buf = (L, j)
+        elif kind == 1:                            # synchronous, device buffer: staged into the input buffer
+            r = fa.CommitResult()
+            ctx._check(ctx.lib.fri_commit_device(ctx.h, ctypes.c_void_p(dev.data_ptr()), d, L, fa.GENERATOR,
+                                                 None, 0, None, ctypes.byref(r)))
+            assert transcript(r) == want
+            self.n_ok += 1
+            self.in_buf = (L, j)
+        elif kind in (2, 3):                       # pipelined, device buffer / host coefficients
+            lane0 = self.next_lane() == 0
+            t = ctx.commit_device_async(dev.data_ptr(), d, L) if kind == 2 else ctx.commit_async(c, L)
+            self.enqueue(t, (L, j))
+            if lane0:
+                self.in_buf = (L, j)               # a lane-0 commit stages its input into the input buffer
+        else:                                      # pipelined, the context's own input buffer
+            p0 = ctypes.c_void_p()
+            ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(p0)))
+            self.enqueue(ctx.commit_device_async(p0.value, d, L), self.in_buf)
+        kinds[kind] = kinds.get(kind, 0) + 1
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--commits", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--contexts", type=int, default=1)
     a = ap.parse_args(argv)
     import torch
     import fri_amd
     import fri_oracle as fo
     corc = fo.load_c_oracle()
     rng = np.random.default_rng(a.seed)
-    shapes = [16, 18, 20]                          # log_n; d = n / 8
     polys = {}                                     # (log_n, j) -> (host u32, device tensor, transcript)
-    for L in shapes:
+    for L in SHAPES:
         d = (1 << L) >> 3
         for j in range(4):
             c = fo.splitmix64_np(7000 + 10 * L + j, d).astype(np.uint32)
             dev = torch.from_numpy(c.view(np.int32).copy()).cuda()
             polys[(L, j)] = (c, dev, oracle_transcript(corc, fo, c, L))
-    ctx = fri_amd.Context(0, max(shapes))
-    lanes = 3
-    ctx.set_lanes(lanes)
-    slots = {}                                     # ticket -> result slot (lowest free slot, fri_api.hip async_enqueue)
-    L = shapes[0]
-    in_buf = None                                  # (log_n, poly index) the input buffer holds, in call order
-    pend = []                                      # (ticket, expected transcript key)
-    n_ok = 0
+    cx = [Driven(fri_amd, polys, rng) for _ in range(a.contexts)]
     kinds = {}
     t0 = time.time()
-
-    def next_lane():
-        return min(set(range(fri_amd.MAX_INFLIGHT)) - set(slots.values())) % lanes
-
-    def enqueue(t, key):
-        slots[t] = min(set(range(fri_amd.MAX_INFLIGHT)) - set(slots.values()))
-        pend.append((t, key))
-
-    def expect(t, key):
-        nonlocal n_ok
-        slots.pop(t)
-        r = ctx.commit_wait(t)
-        assert transcript(r) == polys[key][2], f"pipelined commit of {key} gave a wrong transcript"
-        n_ok += 1
-
-    def drain():
-        while pend:
-            expect(*pend.pop(0))
-
     for i in range(a.commits):
-        u = rng.random()
-        if u < 0.02:                               # another shape: the plans of every lane are rebuilt
-            drain()
-            L = int(rng.choice(shapes))
-            in_buf = None
-        elif u < 0.04:                             # another number of lanes (no commit may be pending)
-            drain()
-            lanes = int(rng.integers(1, fri_amd.MAX_INFLIGHT + 1))
-            ctx.set_lanes(lanes)
-        d = (1 << L) >> 3
-        j = int(rng.integers(0, 4))
-        kind = int(rng.integers(0, 5))
-        if kind == 4 and in_buf is None:
-            kind = 0
-        if len(pend) == fri_amd.MAX_INFLIGHT:
-            expect(*pend.pop(0))
-        c, dev, want = polys[(L, j)]
-        if kind == 0:                              # synchronous, host coefficients: stages them (lane 0)
-            assert transcript(ctx.commit(c, L)) == want
-            n_ok += 1
-            in_buf = (L, j)
-        elif kind == 1:                            # synchronous, device buffer: staged into the input buffer
-            r = fri_amd.CommitResult()
-            ctx._check(ctx.lib.fri_commit_device(ctx.h, ctypes.c_void_p(dev.data_ptr()), d, L, fri_amd.GENERATOR,
-                                                 None, 0, None, ctypes.byref(r)))
-            assert transcript(r) == want
-            n_ok += 1
-            in_buf = (L, j)
-        elif kind == 2:                            # pipelined, device buffer
-            slot_lane0 = next_lane() == 0
-            enqueue(ctx.commit_device_async(dev.data_ptr(), d, L), (L, j))
-            if slot_lane0:
-                in_buf = (L, j)                    # a lane-0 commit stages it into the input buffer
-        elif kind == 3:                            # pipelined, host coefficients (per-slot pinned copy)
-            slot_lane0 = next_lane() == 0
-            enqueue(ctx.commit_async(c, L), (L, j))
-            if slot_lane0:
-                in_buf = (L, j)
-        else:                                      # pipelined, the context's own input buffer
-            p0 = ctypes.c_void_p()
-            ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(p0)))
-            enqueue(ctx.commit_device_async(p0.value, d, L), in_buf)
-        kinds[kind] = kinds.get(kind, 0) + 1
+        cx[int(rng.integers(0, len(cx)))].step(kinds)
         if i % 500 == 0:
-            print(f"[soak] {i} commits, {n_ok} checked, {time.time() - t0:.1f} s", flush=True)
-    drain()
-    ctx.close()
-    print(f"soak ok: {n_ok} commits checked against the C oracle in {time.time() - t0:.1f} s "
+            print(f"[soak] {i} commits, {sum(c.n_ok for c in cx)} checked, {time.time() - t0:.1f} s", flush=True)
+    for c in cx:
+        c.drain()
+        c.ctx.close()
+    n_ok = sum(c.n_ok for c in cx)
+    print(f"soak ok: {n_ok} commits on {len(cx)} context(s) checked against the C oracle in {time.time() - t0:.1f} s "
           f"(kinds: sync-host {kinds.get(0, 0)}, sync-device {kinds.get(1, 0)}, async-device {kinds.get(2, 0)}, "
           f"async-host {kinds.get(3, 0)}, async-input-buffer {kinds.get(4, 0)})", flush=True)
     return n_ok, kinds
