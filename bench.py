@@ -101,6 +101,54 @@ def agree_step(dist, world, rank, step, what):
     return False, note
 
 
+def _host_transport_check(fri_amd, ctx, dist, world, rank, logG, args, agree, timed, attached):
+    """After an RCCL setup failure: the 2^24 codeword (and 2^(24 + log2 N)
+    when it fits the context) committed coset-sharded over the host-staged
+    gloo transport, checked against the oracle's transcript and timed for a
+    few steps (bench.py's own N > 1 protocol, every step agreed over gloo).
+    Returns the record for scaling_points (or the step that failed)."""
+    out = {"transport": "host-staged gloo (RCCL setup failed)", "what": "correctness of the coset-sharded path "
+           "across these GPUs; every collective goes through host memory, so the time is not a scaling figure"}
+    if attached:
+        try:
+            ctx.detach()
+        except fri_amd.FriError:
+            pass
+    ok, msg = agree(dist, world, rank, lambda: ctx.attach_torch(rank, world), "attach (host)")
+    if ok:
+        ok, msg = agree(dist, world, rank, lambda: ctx.dist_selftest(1024), "host transport self-test")
+    if not ok:
+        out["error"] = msg
+        return out
+    points = []
+    for L in (24, 24 + logG):
+        if L - logG <= ctx.log_n_max and L not in points:
+            points.append(L)
+    for L in points:
+        dL = 1 << (L - args.blowup_log)
+        cf = _coeffs(42, dL, fri_amd.P)
+        exp = _expected(L, args.blowup_log)
+        got = {}
+
+        def first():
+            got["r"] = ctx.commit_sharded(cf, L)
+            return True if exp is None else _matches(got["r"], exp)
+
+        ok, msg = agree(dist, world, rank, first, f"host-transport sharded commit 2^{L}")
+        if not ok:
+            out[f"2^{L}"] = {"error": msg}
+            continue
+        k = 3
+        el = timed(lambda: ctx.commit_sharded(cf, L), k, 0)
+        out[f"2^{L}"] = {"codeword_log2": L, "per_gpu_log2": L - logG, "ms_per_step": round(1000 * el / k, 4),
+                         "steps": k, "oracle_verified": exp is not None}
+    try:
+        ctx.detach()
+    except fri_amd.FriError:
+        pass
+    return out
+
+
 def _expected(log_n, blowup_log):
     """Oracle transcript of the bench workload (tests/golden/bench_transcripts.json,
     written by tests/golden/make_bench_transcripts.py from the C oracle), or None."""
@@ -219,11 +267,14 @@ def main():
             uid = torch.frombuffer(bytearray(fri_amd.Context.unique_id()), dtype=torch.uint8).clone()
         dist.broadcast(uid, 0)
 
+        failed_step = None
+
         def agreed(step, what):
-            nonlocal note
+            nonlocal note, failed_step
             ok, msg = agree_step(dist, world, rank, step, what)
             if not ok:
                 note = msg
+                failed_step = failed_step or what
             return ok
 
         attached = False
@@ -279,6 +330,15 @@ def main():
             secondary[name] = {"codeword_log2": L, "per_gpu_log2": L - logG, "ms_per_step": round(1000 * el / k, 4),
                                "value": round((1 << L) * k / el, 1), "unit": "field-elems/s", "steps": k,
                                "oracle_verified": exp is not None and _same(out, first) and _matches(out, exp)}
+        if not ok and args.transport == "rccl" and failed_step in ("attach (rccl)", "transport self-test"):
+            # The RCCL transport itself failed to come up: before the replicas,
+            # run the sharded commit once more over the host-staged gloo
+            # transport (slow: every collective goes through host memory), so
+            # the line still shows whether the coset-sharded path reproduces
+            # the oracle's transcript across these GPUs.  Never `value`.
+            secondary["sharded_host_transport"] = _host_transport_check(
+                fri_amd, ctx, dist, world, rank, logG, args, agree_step, timed, attached)
+            attached = False
         if not ok:
             fallback = note or "the sharded setup failed"
             print(f"[bench] rank {rank}: {fallback}; falling back to replicas", file=sys.stderr, flush=True)
@@ -290,7 +350,7 @@ def main():
             ctx.close()
             mode = "replicas"
             scaling = "weak"
-            secondary = {}
+            secondary = {k: v for k, v in secondary.items() if k == "sharded_host_transport"}
     if mode != "sharded":
         log_n = args.log_n or 24
         d = 1 << (log_n - args.blowup_log)
