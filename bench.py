@@ -330,12 +330,13 @@ def main():
             secondary[name] = {"codeword_log2": L, "per_gpu_log2": L - logG, "ms_per_step": round(1000 * el / k, 4),
                                "value": round((1 << L) * k / el, 1), "unit": "field-elems/s", "steps": k,
                                "oracle_verified": exp is not None and _same(out, first) and _matches(out, exp)}
-        if not ok and args.transport == "rccl" and failed_step in ("attach (rccl)", "transport self-test"):
-            # The RCCL transport itself failed to come up: before the replicas,
-            # run the sharded commit once more over the host-staged gloo
-            # transport (slow: every collective goes through host memory), so
-            # the line still shows whether the coset-sharded path reproduces
-            # the oracle's transcript across these GPUs.  Never `value`.
+        if not ok and args.transport == "rccl" and failed_step is not None:
+            # The RCCL run failed (setup, self-test or the first commit):
+            # before the replicas, run the sharded commit once more over the
+            # host-staged gloo transport (slow: every collective goes through
+            # host memory), so the line still shows whether the coset-sharded
+            # path reproduces the oracle's transcript across these GPUs, i.e.
+            # whether the failure is RCCL's or the protocol's.  Never `value`.
             secondary["sharded_host_transport"] = _host_transport_check(
                 fri_amd, ctx, dist, world, rank, logG, args, agree_step, timed, attached)
             attached = False
