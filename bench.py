@@ -101,19 +101,14 @@ def agree_step(dist, world, rank, step, what):
     return False, note
 
 
-def _host_transport_check(fri_amd, ctx, dist, world, rank, logG, args, agree, timed, attached):
+def _host_transport_check(fri_amd, ctx, dist, world, rank, logG, args, agree, timed):
     """After an RCCL setup failure: the 2^24 codeword (and 2^(24 + log2 N)
     when it fits the context) committed coset-sharded over the host-staged
     gloo transport, checked against the oracle's transcript and timed for a
     few steps (bench.py's own N > 1 protocol, every step agreed over gloo).
     Returns the record for scaling_points (or the step that failed)."""
-    out = {"transport": "host-staged gloo (RCCL setup failed)", "what": "correctness of the coset-sharded path "
+    out = {"transport": "host-staged gloo (the RCCL run failed)", "what": "correctness of the coset-sharded path "
            "across these GPUs; every collective goes through host memory, so the time is not a scaling figure"}
-    if attached:
-        try:
-            ctx.detach()
-        except fri_amd.FriError:
-            pass
     ok, msg = agree(dist, world, rank, lambda: ctx.attach_torch(rank, world), "attach (host)")
     if ok:
         ok, msg = agree(dist, world, rank, lambda: ctx.dist_selftest(1024), "host transport self-test")
@@ -337,9 +332,21 @@ def main():
             # host memory), so the line still shows whether the coset-sharded
             # path reproduces the oracle's transcript across these GPUs, i.e.
             # whether the failure is RCCL's or the protocol's.  Never `value`.
-            secondary["sharded_host_transport"] = _host_transport_check(
-                fri_amd, ctx, dist, world, rank, logG, args, agree_step, timed, attached)
-            attached = False
+            if attached:
+                try:
+                    ctx.detach()
+                except fri_amd.FriError:
+                    pass
+                attached = False
+            if "still busy" in (note or ""):
+                # a stream that did not drain after the RCCL abort: no more work on this device
+                secondary["sharded_host_transport"] = {"skipped": "a stream stayed busy after the RCCL abort"}
+            else:
+                log_n_max = ctx.log_n_max
+                ctx.close()                        # a fresh context for the check (its own streams)
+                ctx = fri_amd.Context(device, log_n_max)
+                secondary["sharded_host_transport"] = _host_transport_check(
+                    fri_amd, ctx, dist, world, rank, logG, args, agree_step, timed)
         if not ok:
             fallback = note or "the sharded setup failed"
             print(f"[bench] rank {rank}: {fallback}; falling back to replicas", file=sys.stderr, flush=True)
