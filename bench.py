@@ -198,6 +198,10 @@ def main():
     dist = None
     device = local_rank
     if world > 1:
+        # one node: RCCL's bootstrap over the loopback interface (the data path
+        # is P2P over xGMI either way; the container's other interfaces and
+        # its hostname may not be routable / resolvable), unless set already
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         import torch
         import torch.distributed as dist
         ndev = torch.cuda.device_count()          # does not initialise HIP
