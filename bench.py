@@ -1047,6 +1047,8 @@ def _cpu_baseline(coeffs, d, log_n):
     return {"value": round((1 << log_n) / t_fast, 1), "unit": "field-elems/s", "cores": nthreads,
             "kind": "port", "host": host, "oracle_verified": fast_ok,
             "cpu_share": {"threads": nthreads, "source": "OMP_NUM_THREADS (the GPU box's host-CPU share per GPU)"},
+            "sha256": ("x86 SHA extensions (as the reference's sha2 0.10.8 selects at run time)"
+                       if lib.orc_sha_backend() else "portable FIPS 180-4 code (no SHA extensions on this CPU)"),
             "all_cores": all_cores,
             "sample": f"full workload: OpenMP C restatement (NTT LDE, eval-form fold, SHA-256 Merkle, channel) "
                       f"at codeword 2^{log_n} on the box's {nthreads}-thread CPU share, median of 5 runs after "

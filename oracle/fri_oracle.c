@@ -238,7 +238,7 @@ static const uint32_t SHA_IV[8] = {0x6a09e667u,0xbb67ae85u,0x3c6ef372u,0xa54ff53
                                    0x510e527fu,0x9b05688cu,0x1f83d9abu,0x5be0cd19u};
 #define ROTR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
 
-static void sha_compress(uint32_t st[8], const uint8_t blk[64]) {
+static void sha_compress_portable(uint32_t st[8], const uint8_t blk[64]) {
     uint32_t w[64];
     for (int t = 0; t < 16; t++)
         w[t] = ((uint32_t)blk[4*t] << 24) | ((uint32_t)blk[4*t+1] << 16) | ((uint32_t)blk[4*t+2] << 8) | blk[4*t+3];
@@ -258,6 +258,70 @@ static void sha_compress(uint32_t st[8], const uint8_t blk[64]) {
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+#if defined(__x86_64__)
+#include <cpuid.h>
+#include <immintrin.h>
+/* The same compression with the x86 SHA extensions.  The reference's SHA-256
+ * (sha2 0.10.8, also under sha256 1.5.0) selects its x86 SHA-NI backend at run
+ * time (cpufeatures) on CPUs that have it, as the GPU box's EPYC does, so the
+ * CPU baseline's port does the same; orc_sha_backend() reports which one runs
+ * and ORC_NO_SHANI=1 forces the portable code (tests check that both agree).
+ * State as the instructions want it: ABEF = {F,E,B,A}, CDGH = {H,G,D,C}. */
+__attribute__((target("sha,sse4.1,ssse3")))
+static void sha_compress_shani(uint32_t st[8], const uint8_t blk[64]) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bLL, 0x0405060700010203LL);
+    const __m128i abcd = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)st), 0xB1);
+    const __m128i efgh = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)(st + 4)), 0x1B);
+    __m128i abef = _mm_alignr_epi8(abcd, efgh, 8);
+    __m128i cdgh = _mm_blend_epi16(efgh, abcd, 0xF0);
+    const __m128i abef0 = abef, cdgh0 = cdgh;
+    __m128i m[4];
+    for (int j = 0; j < 4; j++) m[j] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(blk + 16 * j)), bswap);
+    for (int g = 0; g < 16; g++) {
+        if (g >= 4) {   /* W[t] = s1(W[t-2]) + W[t-7] + s0(W[t-15]) + W[t-16] */
+            __m128i x = _mm_sha256msg1_epu32(m[g & 3], m[(g + 1) & 3]);
+            x = _mm_add_epi32(x, _mm_alignr_epi8(m[(g + 3) & 3], m[(g + 2) & 3], 4));
+            m[g & 3] = _mm_sha256msg2_epu32(x, m[(g + 3) & 3]);
+        }
+        __m128i wk = _mm_add_epi32(m[g & 3], _mm_loadu_si128((const __m128i*)(SHA_K + 4 * g)));
+        cdgh = _mm_sha256rnds2_epu32(cdgh, abef, wk);
+        wk = _mm_shuffle_epi32(wk, 0x0E);
+        abef = _mm_sha256rnds2_epu32(abef, cdgh, wk);
+    }
+    abef = _mm_add_epi32(abef, abef0);
+    cdgh = _mm_add_epi32(cdgh, cdgh0);
+    const __m128i feba = _mm_shuffle_epi32(abef, 0x1B);
+    const __m128i dchg = _mm_shuffle_epi32(cdgh, 0xB1);
+    _mm_storeu_si128((__m128i*)st, _mm_blend_epi16(feba, dchg, 0xF0));
+    _mm_storeu_si128((__m128i*)(st + 4), _mm_alignr_epi8(dchg, feba, 8));
+}
+static int orc_shani_on(void) {
+    static int on = -1;            /* set once; every thread computes the same value */
+    if (on < 0) {
+        unsigned a = 0, b = 0, c = 0, d = 0;
+        const int has = __get_cpuid_count(7, 0, &a, &b, &c, &d) && ((b >> 29) & 1u);
+        const char* e = getenv("ORC_NO_SHANI");
+        on = has && !(e && e[0] && e[0] != '0');
+    }
+    return on;
+}
+#else
+static int orc_shani_on(void) { return 0; }
+#endif
+
+/* 1: the SHA extensions, 0: the portable restatement of FIPS 180-4 */
+int orc_sha_backend(void) { return orc_shani_on(); }
+
+static void sha_compress(uint32_t st[8], const uint8_t blk[64]) {
+#if defined(__x86_64__)
+    if (orc_shani_on()) {
+        sha_compress_shani(st, blk);
+        return;
+    }
+#endif
+    sha_compress_portable(st, blk);
 }
 
 void orc_sha256(const uint8_t* msg, size_t len, uint8_t out[32]) {
