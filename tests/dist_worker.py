@@ -85,6 +85,20 @@ def fuzz_case(i, world):
     return log_n, c, offset, state
 
 
+def fuzz_forced_betas(i):
+    """Forced betas (the FRI_FLAG_FORCE_BETAS test hook) for every third
+    fuzz case, a third of them zero: beta = 0 keeps the odd part's degree in
+    the reference's untrimmed scalar_mul (src/polynomial/ops.rs:87-98), which
+    the sharded degree bookkeeping must reproduce from the chunk maxima."""
+    import numpy as np
+    if i % 3:
+        return None
+    r = np.random.default_rng(90000 + i)
+    fb = r.integers(1, 3221225473, size=32, dtype=np.uint64)
+    fb[r.random(32) < 0.34] = 0
+    return [int(x) for x in fb]
+
+
 def main():
     mode, log_n, seed, out_dir = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     blowup_log = int(sys.argv[5]) if len(sys.argv) > 5 else 3
@@ -102,8 +116,9 @@ def main():
         cases = []
         for i in range(log_n):                         # LOG_N = number of cases
             ln, c, offset, state = fuzz_case(seed + i, world)
+            fb = fuzz_forced_betas(seed + i)
             try:
-                r = ctx.commit_sharded(c.astype(np.uint32), ln, offset, channel_state=state)
+                r = ctx.commit_sharded(c.astype(np.uint32), ln, offset, channel_state=state, forced_betas=fb)
             except fri_amd.FriError as e:
                 cases.append({"error": f"{e.code}: {e}"})
                 continue

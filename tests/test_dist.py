@@ -149,7 +149,8 @@ def test_sharded_fuzz_vs_c_oracle(world, n_cases, corc, oracle):
     """Randomised sharded commits (dist_worker.fuzz_case: 2^20..2^22, ragged
     coefficient counts including 0, blowups 1..16, degrees that end the commit
     inside the sharded layers, zero / constant / odd-only / trailing-zero
-    polynomials, random cosets, prefilled channels) on W ranks sharing GPU 0:
+    polynomials, random cosets, prefilled channels, and for every third case
+    forced betas with zeros among them) on W ranks sharing GPU 0:
     every root, beta, the final value and degree and the channel state equal
     the OpenMP C oracle's 1-node commit (orc_fri_commit_fast, which follows
     src/fri/fri_commit.rs:72-122), on every rank, and every case's transport
@@ -157,11 +158,16 @@ def test_sharded_fuzz_vs_c_oracle(world, n_cases, corc, oracle):
     import ctypes
 
     import numpy as np
-    from dist_worker import fuzz_case
+    from dist_worker import fuzz_case, fuzz_forced_betas
     seed = 100 * world
     got = run_ranks("gpu_fuzz", world, n_cases, seed, timeout=900)
     for i in range(n_cases):
         log_n, c, offset, state = fuzz_case(seed + i, world)
+        fb = fuzz_forced_betas(seed + i)
+        fbp = None
+        if fb is not None:
+            fba = np.ascontiguousarray(np.array(fb, dtype=np.uint64))
+            fbp = fba.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
         d = c.size
         cs = np.ascontiguousarray(c, dtype=np.uint64)
         och = oracle.OrcChannel()
@@ -171,8 +177,9 @@ def test_sharded_fuzz_vs_c_oracle(world, n_cases, corc, oracle):
             och.state_len = 64
         ores = oracle.OrcFriResult()
         assert corc.orc_fri_commit_fast(cs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), d, log_n, offset, 5,
-                                        oracle.P, ctypes.byref(och), None, ctypes.byref(ores), None, None) == 0
-        what = f"case {seed + i}: world={world} log_n={log_n} d={d} offset={offset} prefilled={state is not None}"
+                                        oracle.P, ctypes.byref(och), fbp, ctypes.byref(ores), None, None) == 0
+        what = (f"case {seed + i}: world={world} log_n={log_n} d={d} offset={offset} prefilled={state is not None} "
+                f"forced={fb is not None}")
         want = {"roots": [bytes(ores.roots[k]).hex() for k in range(ores.n_layers)],
                 "betas": [ores.betas[j] for j in range(ores.n_rounds)],
                 "final_value": ores.final_value, "final_degree": ores.final_degree, "state": och.state.decode()}
