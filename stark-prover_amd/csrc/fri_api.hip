@@ -357,9 +357,12 @@ static void plan_free(fri_ctx* ctx) {
 static int use_lane(fri_ctx* ctx, int j) {
     if (j == ctx->cur_lane) return FRI_OK;
     Lane& dst = ctx->lanes[j];
-    if (!dst.stream) {
-        FRI_HIP(ctx, hipStreamCreateWithFlags(&dst.stream, hipStreamNonBlocking));
-        if (dalloc(ctx, &dst.d_state, sizeof(DevState)) != hipSuccess) return fail(ctx, FRI_ENOMEM, "lane state");
+    // (each part on its own: a lane whose state allocation failed once gets
+    // it on the next use, instead of being installed with a null state)
+    if (!dst.stream) FRI_HIP(ctx, hipStreamCreateWithFlags(&dst.stream, hipStreamNonBlocking));
+    if (!dst.d_state && dalloc(ctx, &dst.d_state, sizeof(DevState)) != hipSuccess) {
+        dst.d_state = nullptr;
+        return fail(ctx, FRI_ENOMEM, "lane state");
     }
     Lane& park = ctx->lanes[ctx->cur_lane];
     std::swap(park.plan, ctx->plan);
