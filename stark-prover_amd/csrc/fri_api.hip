@@ -1219,10 +1219,10 @@ static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32
     // this commit's lane (its own stream, plan and device state): the
     // commits pending on other lanes run beside it
     if ((rv = use_lane(ctx, slot % ctx->max_lanes))) return rv;
-    if (!ctx->h_slot[slot]) {
-        FRI_HIP(ctx, hipHostMalloc(&ctx->h_slot[slot], sizeof(DevState), hipHostMallocDefault));
-        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_slot[slot], hipEventDisableTiming));
-    }
+    // (each lazily created member on its own: one whose creation failed is
+    // created on the next call instead of being used null)
+    if (!ctx->h_slot[slot]) FRI_HIP(ctx, hipHostMalloc(&ctx->h_slot[slot], sizeof(DevState), hipHostMallocDefault));
+    if (!ctx->ev_slot[slot]) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_slot[slot], hipEventDisableTiming));
     // (every argument check ran before the pinned copy and the upload: a
     // commit refused later would leave the slot free with its upload in flight)
     if (host_coeffs && d) {
@@ -1395,8 +1395,8 @@ extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint3
 // of that size took either ~25 or ~130 us per query, varying from process to
 // process; the zero-copy write does not go through the copy engines).
 static int dq_alloc(fri_ctx* ctx) {
-    if (!ctx->dq_host) {
-        FRI_HIP(ctx, hipHostMalloc(&ctx->dq_host, 65536, hipHostMallocMapped | hipHostMallocCoherent));
+    if (!ctx->dq_host) FRI_HIP(ctx, hipHostMalloc(&ctx->dq_host, 65536, hipHostMallocMapped | hipHostMallocCoherent));
+    if (!ctx->dq_dev) {
         void* d = nullptr;
         FRI_HIP(ctx, hipHostGetDevicePointer(&d, ctx->dq_host, 0));
         ctx->dq_dev = static_cast<uint32_t*>(d);
@@ -1587,10 +1587,12 @@ extern "C" int fri_debug_inject_stall(fri_ctx* ctx, int enable) {
     if (!ctx) return FRI_EINVAL;
     if (!ctx->stall_flag) {
         FRI_HIP(ctx, hipHostMalloc(&ctx->stall_flag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        *ctx->stall_flag = 1u;
+    }
+    if (!ctx->stall_flag_dev) {
         void* d = nullptr;
         FRI_HIP(ctx, hipHostGetDevicePointer(&d, ctx->stall_flag, 0));
         ctx->stall_flag_dev = static_cast<uint32_t*>(d);
-        *ctx->stall_flag = 1u;
     }
     ctx->inject_stall = enable != 0;
     return FRI_OK;
@@ -2022,14 +2024,14 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
         FRI_HIP(ctx, dalloc(ctx, &b.half, (M / 2 + 1) * 4));
         b.cap = M;
     }
-    if (!b.top) {
-        FRI_HIP(ctx, dalloc(ctx, &b.top, (size_t)(MAXR + 1) * 2 * 64 * 32));
-        FRI_HIP(ctx, dalloc(ctx, &b.pre_lo, ((size_t)1 << POW_LO_LOG) * 4));
-        FRI_HIP(ctx, dalloc(ctx, &b.pre_hi, nhi * 4));
-    }
-    if (!b.rec) {
-        FRI_HIP(ctx, dalloc(ctx, &b.rec, (size_t)(64 + 1) * REC_WORDS * 4));
+    // (each lazily created member on its own, as in async_enqueue)
+    if (!b.top) FRI_HIP(ctx, dalloc(ctx, &b.top, (size_t)(MAXR + 1) * 2 * 64 * 32));
+    if (!b.pre_lo) FRI_HIP(ctx, dalloc(ctx, &b.pre_lo, ((size_t)1 << POW_LO_LOG) * 4));
+    if (!b.pre_hi) FRI_HIP(ctx, dalloc(ctx, &b.pre_hi, nhi * 4));
+    if (!b.rec) FRI_HIP(ctx, dalloc(ctx, &b.rec, (size_t)(64 + 1) * REC_WORDS * 4));
+    if (!b.shtop) {
         FRI_HIP(ctx, dalloc(ctx, &b.shtop, (size_t)(MAXR + 1) * sizeof(ShardTop)));
+        b.shtop_h.clear();                 // a new table buffer: upload on the next sharded call
     }
     if (b.gcap < gwords) {
         dfree(ctx, b.gath);
@@ -2037,16 +2039,12 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
         FRI_HIP(ctx, dalloc(ctx, &b.gath, gwords * 4));
         b.gcap = gwords;
     }
-    if (!ctx->xstream) {
-        FRI_HIP(ctx, hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking));
-        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_vals, hipEventDisableTiming));
-        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_xchg, hipEventDisableTiming));
-    }
-    if (!ctx->cstream) {
-        FRI_HIP(ctx, hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
-        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_pre, hipEventDisableTiming));
-        FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_coef, hipEventDisableTiming));
-    }
+    if (!ctx->xstream) FRI_HIP(ctx, hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking));
+    if (!ctx->ev_vals) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_vals, hipEventDisableTiming));
+    if (!ctx->ev_xchg) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_xchg, hipEventDisableTiming));
+    if (!ctx->cstream) FRI_HIP(ctx, hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
+    if (!ctx->ev_pre) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_pre, hipEventDisableTiming));
+    if (!ctx->ev_coef) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_coef, hipEventDisableTiming));
     (void)G;
     return FRI_OK;
 }
