@@ -947,8 +947,9 @@ def fri_commit_pipelined(polys: Sequence[Sequence[int]], log_n: int, channels: S
     """fri_commit (fri_commit.rs:72-122) of many polynomials in a row, each
     with its own channel, pipelined from this one host thread
     (fri_commit_async / fri_commit_wait, ``depth`` commits in flight per
-    context, each on a commit lane of its own: one context overlaps them).  ``ctx`` is one Context or a list of them: with several, the
-    commits are dealt round-robin and run concurrently, one stream each.
+    context, each on a commit lane of its own: one context overlaps them).
+    ``ctx`` is one Context or a list of them: with several, the commits are
+    dealt round-robin and run concurrently, one stream each.
     Proof i equals fri_commit of polys[i] into channels[i]; on each context
     only its last proof's layers stay resident."""
     if len(polys) != len(channels):
