@@ -7,6 +7,10 @@ MODE "model": CPU model of the sharded commit (tests/dist_model.py) with the
               C oracle doing the per-block work and gloo doing the exchanges.
 MODE "gpu":   libfri_amd.so fri_commit_sharded on GPU 0 (every rank shares
               the one GPU), collectives staged through the host over gloo.
+MODE "gpu_soak": LOG_N operations on one context per rank: sharded commits
+              (collective, the same sequence on every rank) mixed with this
+              rank's own synchronous and pipelined 1-GPU commits, every
+              transcript checked against the C oracle's.
 MODE "gpu_fuzz": LOG_N random sharded commits (fuzz_case(SEED + i, W): ragged
               coefficient counts, blowups 1..16, early-ending and zero
               polynomials, random cosets, prefilled channels), one result per
@@ -109,6 +113,70 @@ def main():
     import numpy as np
 
     import fri_oracle as fo
+    if mode == "gpu_soak":
+        # LOG_N = number of operations; the operation sequence is drawn from
+        # SEED on every rank alike (sharded commits are collective), the
+        # polynomials of the local commits from SEED + rank (they differ per rank)
+        import ctypes
+        import fri_amd
+        corc = fo.load_c_oracle()
+
+        def oracle_t(c, L):
+            cs = np.ascontiguousarray(c, dtype=np.uint64)
+            och = fo.OrcChannel()
+            corc.orc_channel_init(ctypes.byref(och))
+            res = fo.OrcFriResult()
+            assert corc.orc_fri_commit_fast(cs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), c.size, L, 5, 5, fo.P,
+                                            ctypes.byref(och), None, ctypes.byref(res), None, None) == 0
+            return [bytes(res.roots[k]).hex() for k in range(res.n_layers)], och.state.decode()
+
+        def got_t(r):
+            return [bytes(r.roots[k]).hex() for k in range(r.n_layers)], bytes(r.channel_out.digest).hex()
+
+        polys = {}
+        for L in (20, 21, 14, 16):
+            for j in range(2):
+                c = fo.splitmix64_np(8000 + 10 * L + j + (0 if L >= 20 else 100 * (rank + 1)), (1 << L) >> 3)
+                polys[(L, j)] = (c.astype(np.uint32), oracle_t(c, L))
+        ctx = fri_amd.Context(0, 21)
+        ctx.attach_torch(rank, world)
+        ctx.set_lanes(3)
+        seq = np.random.default_rng(seed)            # same on every rank
+        loc = np.random.default_rng(seed + 1 + rank)  # this rank's local choices
+        pend, counts, bad = [], {"sharded": 0, "sync": 0, "async": 0}, []
+
+        def wait_one():
+            t, key = pend.pop(0)
+            if got_t(ctx.commit_wait(t)) != polys[key][1]:
+                bad.append(("async", key))
+
+        for i in range(log_n):
+            if seq.random() < 0.3:
+                L, j = int(seq.choice([20, 21])), int(seq.integers(0, 2))
+                r = ctx.commit_sharded(polys[(L, j)][0], L)
+                counts["sharded"] += 1
+                if got_t(r) != polys[(L, j)][1]:
+                    bad.append(("sharded", L, j))
+            else:
+                L, j = int(loc.choice([14, 16])), int(loc.integers(0, 2))
+                if loc.random() < 0.5:
+                    counts["sync"] += 1
+                    if got_t(ctx.commit(polys[(L, j)][0], L)) != polys[(L, j)][1]:
+                        bad.append(("sync", L, j))
+                else:
+                    if len(pend) == fri_amd.MAX_INFLIGHT:
+                        wait_one()
+                    pend.append((ctx.commit_async(polys[(L, j)][0], L), (L, j)))
+                    counts["async"] += 1
+        while pend:
+            wait_one()
+        ctx.detach()
+        ctx.close()
+        with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+            json.dump({"counts": counts, "bad": bad}, f)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     if mode == "gpu_fuzz":
         import fri_amd
         ctx = fri_amd.Context(0, 22)

@@ -191,6 +191,21 @@ def test_sharded_fuzz_vs_c_oracle(world, n_cases, corc, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_and_local_commits_mixed(world):
+    """One context per rank alternating at random between sharded commits
+    (2^20 / 2^21, collective) and the rank's own synchronous and pipelined
+    1-GPU commits (2^14 / 2^16, three commit lanes): every plan switch between
+    the sharded and the 1-GPU shapes frees the lanes' plans behind the
+    pending commits, and every transcript, on every rank, must still equal
+    the C oracle's (src/fri/fri_commit.rs:72-122)."""
+    got = run_ranks("gpu_soak", world, 300, 4242 + world, timeout=900)
+    for r in got:
+        assert r["bad"] == [], r["bad"][:5]
+        assert r["counts"]["sharded"] > 40 and r["counts"]["sync"] > 40 and r["counts"]["async"] > 40, r["counts"]
+
+
+@pytest.mark.gpu
 def test_loopback_rehearsal_transport(oracle):
     """fri_debug_attach_loopback (tools/shard_projection.py): one rank's share
     of a sharded commit runs on one device with every round of the real
