@@ -143,10 +143,10 @@ def test_sharded_commit_gpu_matches_single(world, log_n, blowup_log, kind, corc,
     assert n_main >= 1 and (n_x >= 1 or kind == "low_degree" or log_n - 1 < 20)
 
 
-@pytest.mark.gpu
 _SF = int(os.environ.get("SHARD_FUZZ_N", "0"))      # > 0: that many cases per world size (longer runs)
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("world,n_cases", [(2, _SF or 10), (4, _SF or 10), (8, _SF or 8)])
 def test_sharded_fuzz_vs_c_oracle(world, n_cases, corc, oracle):
     """Randomised sharded commits (dist_worker.fuzz_case: 2^20..2^22, ragged
