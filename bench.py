@@ -162,6 +162,55 @@ def _matches(res, exp):
             and bytes(res.channel_out.digest).hex() == exp["state"])
 
 
+def launch_plan(gpus, env, transport="rccl"):
+    """How `bench.py --gpus N` runs, decided before anything touches the GPU:
+      "run"      - this process is the whole job (N == 1, or --transport p2p:
+                   one process drives the N GPUs as a team context) or one
+                   rank of a launcher's job whose WORLD_SIZE is N;
+      "spawn"    - N > 1 and no launcher: start the N ranks as
+                   `python -m torch.distributed.run` (a child process) and
+                   relay rank 0's JSON line;
+      "mismatch" - a launcher started WORLD_SIZE ranks but --gpus says N:
+                   refuse (a 1-rank job must not be reported as N GPUs)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if gpus > 1 and transport != "p2p" else "run"
+    return "run" if int(ws) == gpus else "mismatch"
+
+
+def spawn_command(gpus, argv, port):
+    """The child launcher of launch_plan's "spawn": one rank per GPU over
+    127.0.0.1 (the container hostname may not resolve)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _spawn_ranks(gpus, argv):
+    """Run the N ranks under torch.distributed.run as a child process (this
+    process never initialises HIP), pass their stderr through and print rank
+    0's JSON line on stdout; exit with the child's status."""
+    cmd = spawn_command(gpus, argv, _free_port())
+    print(f"[bench] --gpus {gpus} without a launcher: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    line = None
+    for ln in proc.stdout.splitlines():
+        try:
+            if "metric" in json.loads(ln):
+                line = ln
+        except ValueError:
+            print(ln, file=sys.stderr)
+    if line is not None:
+        print(line, flush=True)
+    return proc.returncode if line is not None or proc.returncode else 1
+
+
 def main():
     # The contract's ONE JSON line goes to the original stdout; everything
     # else written to fd 1 by native libraries (gloo connection messages, the
@@ -182,8 +231,12 @@ def main():
     ap.add_argument("--blowup-log", type=int, default=3)
     ap.add_argument("--mode", choices=("sharded", "replicas"), default="sharded",
                     help="N>1: one coset-sharded codeword (default), or N independent 2^24 commits")
-    ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
-                    help="sharded data path: the library's RCCL communicator, or host-staged gloo (rehearsal only)")
+    ap.add_argument("--transport", choices=("rccl", "host", "p2p"), default="rccl",
+                    help="sharded data path: the library's RCCL communicator (one process per GPU), host-staged "
+                         "gloo (rehearsal only), or p2p: ONE process drives the N GPUs as a team context "
+                         "(fri_ctx_create_multi, peer transport over xGMI); under a launcher rank 0 runs the team")
+    ap.add_argument("--no-p2p-fallback", action="store_true",
+                    help="N>1 rccl: when the RCCL run fails, go to replicas without trying the p2p team first")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N>1: skip the secondary scaling points (weak 2^24 per GPU, strong 2^24)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -191,6 +244,15 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the side measurements (PCIe-inclusive, serving, prover, 2^28): A/B timing runs")
     args = ap.parse_args()
+    plan = launch_plan(args.gpus, os.environ, args.transport)
+    if plan == "spawn":
+        os.dup2(json_fd, 1)                         # the relayed line goes to the real stdout
+        raise SystemExit(_spawn_ranks(args.gpus, sys.argv[1:]))
+    if plan == "mismatch":
+        msg = f"--gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks"
+        os.write(json_fd, (json.dumps({"metric": METRIC, "value": None, "error": msg}) + "\n").encode())
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+        raise SystemExit(2)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -200,8 +262,10 @@ def main():
     if world > 1:
         # one node: RCCL's bootstrap over the loopback interface (the data path
         # is P2P over xGMI either way; the container's other interfaces and
-        # its hostname may not be routable / resolvable), unless set already
-        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        # its hostname may not be routable / resolvable), unless set already.
+        # A job spread over several nodes keeps RCCL's own interface choice.
+        if int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world:
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         import torch
         import torch.distributed as dist
         ndev = torch.cuda.device_count()          # does not initialise HIP
@@ -214,10 +278,21 @@ def main():
     import numpy as np
     import fri_amd
 
-    logG = world.bit_length() - 1
-    mode = args.mode if world > 1 else "single"
-    if world > 1 and (1 << logG) != world:
+    pg = dist                    # the job's process group (kept when the team runs on rank 0 alone)
+    # --transport p2p: one process drives the N GPUs (a team context); under
+    # a launcher rank 0 drives them all and the other ranks wait for it
+    team_n = (world if world > 1 else args.gpus) if args.transport == "p2p" else 0
+    if team_n and world > 1:
+        if rank != 0:
+            _team_wait(pg)
+            return
+        dist = None
+    ndev_all = _device_count()
+    logG = (team_n or world).bit_length() - 1
+    mode = args.mode if (team_n or world) > 1 else "single"
+    if (team_n or world) > 1 and (1 << logG) != (team_n or world):
         mode = "replicas"                                   # sharding needs a power-of-two world
+        team_n = 0
     scaling = "weak"
     if mode == "sharded":
         scaling = args.scaling if args.scaling != "auto" else ("weak" if args.log_n is not None else "strong")
@@ -252,14 +327,19 @@ def main():
     res = fri_amd.CommitResult()
     secondary = {}
     dist_report = None
-    if mode == "sharded":
+    team_devices = None
+    if mode == "sharded" and team_n:
+        log_n = (args.log_n or 28) if scaling == "strong" else (args.log_n or 24) + logG
+        team_devices = [r % max(ndev_all, 1) for r in range(team_n)]
+        ts = _team_stage(fri_amd, team_devices, _shard_points(args, scaling, log_n, logG), args, timed)
+        ctx, step, res0, res, d, coeffs, verified = (ts[k] for k in ("ctx", "step", "res0", "res", "d", "coeffs",
+                                                                     "verified"))
+        secondary.update(ts["secondary"])
+        dist_report = ts["dist_report"]
+    elif mode == "sharded":
         import torch
         log_n = (args.log_n or 28) if scaling == "strong" else (args.log_n or 24) + logG
-        points = [(f"{scaling}_primary", log_n)]
-        if not args.no_secondary:
-            for name, L in (("weak_2p24_per_gpu", 24 + logG), ("strong_2p24", 24)):
-                if L != log_n:
-                    points.insert(0, (name, L))              # secondaries first: the primary's plan stays resident
+        points = _shard_points(args, scaling, log_n, logG)
         ctx = fri_amd.Context(device, max(L for _, L in points) - logG)   # shard-sized (fri_amd.h)
         uid = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
@@ -353,16 +433,50 @@ def main():
                     fri_amd, ctx, dist, world, rank, logG, args, agree_step, timed)
         if not ok:
             fallback = note or "the sharded setup failed"
-            print(f"[bench] rank {rank}: {fallback}; falling back to replicas", file=sys.stderr, flush=True)
             if attached:
                 try:
                     ctx.detach()
                 except fri_amd.FriError:
                     pass
             ctx.close()
-            mode = "replicas"
-            scaling = "weak"
             secondary = {k: v for k, v in secondary.items() if k == "sharded_host_transport"}
+            team_status = None
+            if args.transport == "rccl" and not args.no_p2p_fallback:
+                # Before the replicas: the same coset-sharded commit driven by
+                # rank 0 alone as a team context over every GPU of the job
+                # (peer transport: device copies over xGMI, no RCCL).  The
+                # other ranks wait for its verdict; on success they wait for
+                # the end of the job, otherwise everyone goes to replicas.
+                print(f"[bench] rank {rank}: {fallback}; trying the p2p team on rank 0", file=sys.stderr, flush=True)
+                ts = None
+                if rank == 0:
+                    team_devices = [r % max(ndev_all, 1) for r in range(world)]
+                    try:
+                        ts = _team_stage(fri_amd, team_devices, _shard_points(args, scaling, log_n, logG), args,
+                                         lambda st, k, w: _plain_timed(st, k, w))
+                        team_status = "ok"
+                    except Exception as e:  # noqa: BLE001 - reported in the line, then replicas
+                        team_status = f"{type(e).__name__}: {e}"
+                box = [team_status]
+                dist.broadcast_object_list(box, src=0)
+                team_status = box[0]
+                if team_status == "ok":
+                    if rank != 0:
+                        _team_wait(pg)
+                        return
+                    dist = None
+                    team_n = world
+                    ctx, step, res0, res, d, coeffs, verified = (ts[k] for k in ("ctx", "step", "res0", "res", "d",
+                                                                                 "coeffs", "verified"))
+                    secondary.update(ts["secondary"])
+                    dist_report = ts["dist_report"]
+                    fallback = f"RCCL run failed ({fallback}); the p2p team on rank 0 ran the sharded commit instead"
+                else:
+                    secondary["sharded_p2p_team"] = {"error": team_status}
+            if team_status != "ok":
+                print(f"[bench] rank {rank}: {fallback}; falling back to replicas", file=sys.stderr, flush=True)
+                mode = "replicas"
+                scaling = "weak"
     if mode != "sharded":
         log_n = args.log_n or 24
         d = 1 << (log_n - args.blowup_log)
@@ -381,6 +495,7 @@ def main():
             ctx._check(ctx.lib.fri_commit_device(ctx.h, dptr, d, log_n, fri_amd.GENERATOR, None, 0, None,
                                                  ctypes.byref(res)))
 
+    solo = world == 1 and not team_n        # one process, one GPU: the side stages run
     elapsed = timed(step, args.steps, args.warmup)
     if args.warmup:
         assert _same(res, res0)
@@ -469,16 +584,16 @@ def main():
     # active stream then has a hardware queue of its own.
     concurrent = None
     pipelined = None
-    if world == 1 and mode == "single" and log_n >= 20 and not args.no_extras:
+    if solo and mode == "single" and log_n >= 20 and not args.no_extras:
         single = _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K=4, steps=max(12, args.steps))
         concurrent = _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C=3, steps=max(5, args.steps // 2))
         concurrent["single_thread_async"] = single
-    if world == 1 and mode == "single" and log_n >= 20 and not args.no_extras:
+    if solo and mode == "single" and log_n >= 20 and not args.no_extras:
         pipelined = _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps=args.steps)
 
     # PCIe-inclusive rate (host coefficients in, result out): never `value`
     pcie = None
-    if world == 1 and not args.no_extras:
+    if solo and not args.no_extras:
         k = max(3, min(args.steps, 10))
         t0 = time.perf_counter()
         for _ in range(k):
@@ -507,14 +622,14 @@ def main():
     # just made: one fri_decommit_query per query index gathers both values and
     # both authentication paths of every layer.  Beside `value`, never it.
     decommit = None
-    if world == 1 and mode == "single" and not args.no_extras:
+    if solo and mode == "single" and not args.no_extras:
         decommit = _decommit_stage(fri_amd, ctx, res, log_n)
 
     # Trace side of the prover (BASELINE configs[3] trace length): 2^16 trace
     # -> iNTT -> coset LDE 2^19 -> Merkle commit, device-resident (reported
     # beside the metric, never `value`).
     trace_stage = None
-    if world == 1 and log_n >= 19 and not args.no_extras:
+    if solo and log_n >= 19 and not args.no_extras:
         tr = _coeffs(7, 1 << 16, fri_amd.P)
         ctx.trace_commit(tr, 3)
         k = 10
@@ -530,31 +645,43 @@ def main():
     # FRI commit -> 3 queries (trace + FRI decommitments); host trace in,
     # transcript out.  Reported beside the metric, never `value`.
     prover = None
-    if world == 1 and log_n >= 19 and not args.no_extras:
+    if solo and log_n >= 19 and not args.no_extras:
         prover = _prover_stage(ctx, fri_amd, with_cpu=(rank == 0 and not args.no_cpu_baseline))
 
     # The 1-GPU point of the 2^28 strong-scaling curve (BASELINE configs[4]'s
     # codeword on one GPU, ~38 GB of HBM), checked against the oracle's
     # transcript.  Beside `value`, never it.
-    if world == 1 and mode == "single" and log_n < 28 and not args.no_extras:
+    if solo and mode == "single" and log_n < 28 and not args.no_extras:
         secondary["single_2p28"] = _single_point(fri_amd, device, 28, args.blowup_log, steps=5)
 
-    hbm = ctx.device_bytes()[1]
-    hbm_max = max_over_ranks(float(hbm))
+    if team_n:                               # a team: the largest rank's HBM
+        hbm_max = float(max(ctx.team_rank(r).device_bytes()[1] for r in range(team_n)))
+    else:
+        hbm_max = max_over_ranks(float(ctx.device_bytes()[1]))
 
     cpu = None
     configs0 = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and solo and not args.no_cpu_baseline:
         cpu = _cpu_baseline(coeffs, d, log_n)
         configs0 = _configs0_stage(ctx)
 
     if rank == 0:
+        # the sharded run's size as its communicator (or the team) reports it
+        n_ranks = (dist_report or {}).get("world_reported", world) if mode == "sharded" else world
         if mode == "sharded":
             workload = (f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} (d=2^{log_n - args.blowup_log}), "
-                        f"coset-sharded over {world} GPUs (2^{blk_log} per GPU), SHA-256 Merkle per layer, "
+                        f"coset-sharded over {n_ranks} GPUs (2^{blk_log} per GPU), SHA-256 Merkle per layer, "
                         f"{res.n_rounds} rounds")
-            par = (f"coset-sharded x{world} (RCCL all-to-all + pair exchange)" if args.transport == "rccl"
-                   else f"coset-sharded x{world} (host-staged gloo transport, rehearsal)")
+            if team_n:
+                nd = len(set(team_devices or []))
+                par = (f"coset-sharded x{n_ranks} in ONE process (team context, peer transport: each collective "
+                       f"one pull kernel over xGMI) on {nd} distinct device(s); the other ranks copy rank 0's "
+                       f"input buffer inside every step")
+                if fallback:
+                    par += f" (FALLBACK: {fallback})"
+            else:
+                par = (f"coset-sharded x{n_ranks} (RCCL all-to-all + pair exchange)" if args.transport == "rccl"
+                       else f"coset-sharded x{n_ranks} (host-staged gloo transport, rehearsal)")
         else:
             workload = (f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} (d=2^{log_n - args.blowup_log}), "
                         f"SHA-256 Merkle per layer, {res.n_rounds} rounds" + (", per GPU" if world > 1 else ""))
@@ -562,7 +689,7 @@ def main():
             if fallback:
                 par += f" (FALLBACK: the coset-sharded path failed: {fallback})"
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "field-elems/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 1), "unit": "field-elems/s", "n_gpus": n_ranks,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 % p coefficients" + (", seed 42)" if mode != "replicas" else ", seed 42+rank)"),
@@ -587,11 +714,90 @@ def main():
         if fallback:
             line["note"] = fallback
         os.write(json_fd, (json.dumps(line) + "\n").encode())
-    if mode == "sharded":
+    if mode == "sharded" and not team_n:
         ctx.detach()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+    elif pg is not None:
+        _team_wait(pg)                   # the ranks that waited for this team run
+
+
+def _device_count():
+    """GPUs visible to this process, without initialising HIP (torch's count
+    does not; 1 when torch is unavailable)."""
+    try:
+        import torch
+        return max(1, torch.cuda.device_count())
+    except Exception:  # noqa: BLE001
+        return 1
+
+
+def _team_wait(pg):
+    """A rank that is not driving the p2p team: wait for rank 0's run to end."""
+    pg.barrier()
+    pg.destroy_process_group()
+
+
+def _plain_timed(step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    return time.perf_counter() - t0
+
+
+def _shard_points(args, scaling, log_n, logG):
+    """The sharded run's codewords: the primary (strong 2^28 / weak 2^24 per
+    GPU) last, so its plan stays resident, after the secondary points."""
+    points = [(f"{scaling}_primary", log_n)]
+    if not args.no_secondary:
+        for name, L in (("weak_2p24_per_gpu", 24 + logG), ("strong_2p24", 24)):
+            if L != log_n:
+                points.insert(0, (name, L))
+    return points
+
+
+def _team_stage(fri_amd, devices, points, args, timed):
+    """The coset-sharded commit over `devices` from THIS process: one team
+    context (fri_ctx_create_multi, peer transport), one fri_commit_device
+    call per step (the single-call surface of fri_commit.rs:72-76).  Inputs
+    resident: rank 0's input buffer, which the other ranks copy over xGMI
+    inside every step.  Each point's first transcript is checked against the
+    C oracle's golden transcript; a mismatch raises."""
+    G = len(devices)
+    logG = G.bit_length() - 1
+    ctx = fri_amd.Context.multi(devices, max(L for _, L in points), transport="peer")
+    r_rank, r_world, r_kind = ctx.dist_info()
+    out = {"ctx": ctx, "secondary": {},
+           "dist_report": {"transport": r_kind, "world_reported": r_world, "rank_reported": r_rank,
+                           "process": "one process drives every rank (team context)", "devices": devices,
+                           "distinct_devices": len(set(devices))}}
+    for name, L in points:
+        dL = 1 << (L - args.blowup_log)
+        cf = _coeffs(42, dL, fri_amd.P)
+        exp = _expected(L, args.blowup_log)
+        first = ctx.commit(cf, L)
+        if exp is not None and not _matches(first, exp):
+            raise RuntimeError(f"team transcript of 2^{L} differs from the C oracle's")
+        dptr = ctypes.c_void_p()
+        ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, dL, ctypes.byref(dptr)))
+        res = fri_amd.CommitResult()
+
+        def step(dptr=dptr, dL=dL, L=L, res=res):
+            ctx._check(ctx.lib.fri_commit_device(ctx.h, dptr, dL, L, fri_amd.GENERATOR, None, 0, None,
+                                                 ctypes.byref(res)))
+
+        if name.endswith("_primary"):
+            out.update(step=step, res0=first, res=res, d=dL, coeffs=cf, verified=exp is not None, log_n=L)
+            break
+        k = max(3, args.steps // 4)
+        el = timed(step, k, 1)
+        out["secondary"][name] = {"codeword_log2": L, "per_gpu_log2": L - logG, "ms_per_step": round(1000 * el / k, 4),
+                                  "value": round((1 << L) * k / el, 1), "unit": "field-elems/s", "steps": k,
+                                  "oracle_verified": exp is not None and _same(res, first) and _matches(res, exp)}
+    return out
 
 
 def _decommit_stage(fri_amd, ctx, res, log_n, nq=64):

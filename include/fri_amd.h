@@ -245,8 +245,12 @@ int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result* out);
 
 /* Commit lanes of pipelined commits.  Each lane is a stream with its own
  * commit plan (input and coefficient buffers, layers, trees, x^-1 tables,
- * graphs, device state); pending commit i goes to lane (result slot mod
- * max_lanes), created on first use.  Commits on different lanes run
+ * graphs, device state), created on first use.  A pipelined commit goes to
+ * the lane with the fewest pending (un-waited) commits, ties to the lane
+ * dealt a commit longest ago (an unused lane first, lower index first); a
+ * lane that gets no HBM for its plan is dropped from the rotation until the
+ * next fri_ctx_set_lanes or plan change (the commit runs on another lane;
+ * FRI_ENOMEM only when lane 0 itself cannot get one).  Commits on different lanes run
  * concurrently, so one commit's serial tree tops (the Fiat-Shamir chain,
  * one workgroup) overlap the next commit's leaf hashing on the otherwise
  * idle chip.  Default FRI_DEFAULT_LANES (3) lanes: a caller keeping k <= 3
@@ -261,6 +265,9 @@ int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result* out);
  * commits are pending. */
 #define FRI_DEFAULT_LANES 3
 int fri_ctx_set_lanes(fri_ctx* ctx, uint32_t max_lanes);
+/* Diagnostic: the lane a pending pipelined commit was dealt to (0-based);
+ * FRI_EINVAL for a ticket that is not pending. */
+int fri_debug_ticket_lane(fri_ctx* ctx, uint64_t ticket, int* lane);
 
 /* Which commit the read-backs below serve: `generation` grows with every
  * commit call on the context (successful or not), log_n / n_layers describe
@@ -291,6 +298,44 @@ int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint32_t* value_
  * *paths_len = total path bytes (also set when paths_cap is too small). */
 int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap,
                        uint8_t* paths, size_t paths_cap, size_t* paths_len);
+
+/* ------------------------------------------- single-process multi-GPU team */
+/* One context over n_devices GPUs, driven by ONE call from ONE host thread:
+ * the reference's fri_commit(poly, domain, &mut channel)
+ * (src/fri/fri_commit.rs:72-76) spread over 1-8 GPUs ("the library drives
+ * 1-8 GPUs from one host thread").  devices: the HIP
+ * ordinals of ranks 0..n-1 (NULL: 0..n-1); an ordinal may repeat (several
+ * ranks on one GPU; peer transport only).  n_devices: a power of two <= 64;
+ * 1 gives an ordinary context.  log_n_max: the largest codeword; every
+ * rank's context is shard-sized (2^(log_n_max - log2 n), and at least
+ * 2^min(log_n_max, 19) for the commits rank 0 runs alone).  transport:
+ *   FRI_TRANSPORT_RCCL  communicators from ncclCommInitAll (xGMI);
+ *   FRI_TRANSPORT_PEER  device copies between the ranks' buffers: one pull
+ *                       kernel per collective reading the other ranks'
+ *                       memory over xGMI peer access, ordered by events;
+ *   FRI_TRANSPORT_NONE  automatic: RCCL when it initialises, else peer.
+ * Inside, rank 0 runs on the calling thread and ranks 1..n-1 on worker
+ * threads of the context (one per rank), each issuing the sharded protocol
+ * of fri_commit_sharded on its device.  The returned context is rank 0's:
+ *   fri_commit / fri_commit_device / fri_commit_sharded*: a codeword of
+ *     >= 2^20 elements (and >= 2^(12 + log2 n)) is committed coset-sharded
+ *     over the ranks in this one call, with the same result and transcript
+ *     as a 1-GPU commit; smaller codewords run on rank 0 alone.
+ *     fri_commit_device reads a buffer on rank 0's device (the other ranks
+ *     copy it over xGMI);
+ *   fri_layer_copy / fri_tree_level_copy / fri_auth_path / fri_decommit_query
+ *     (and _sharded) serve every layer: the sharded ones are assembled from
+ *     the ranks' blocks and the replicated top trees;
+ *   fri_ctx_device_bytes: the sum over the ranks;
+ *   the kernel-level calls (fri_lde, fri_merkle_root, ...) run on rank 0;
+ *   fri_commit_*async and fri_dist_attach_* / fri_dist_detach: FRI_EINVAL.
+ * Not re-entrant (one host thread at a time), like every context.
+ * fri_ctx_destroy(ctx) releases every rank. */
+int fri_ctx_create_multi(const int* devices, uint32_t n_devices, uint32_t log_n_max, int transport, fri_ctx** out);
+/* Diagnostic: rank `rank`'s context of a team (rank 0: ctx itself), e.g. for
+ * its fri_debug_transport_log; owned by the team, never destroyed by the
+ * caller (FRI_EINVAL). */
+int fri_debug_team_rank(fri_ctx* ctx, uint32_t rank, fri_ctx** out);
 
 /* -------------------------------------------------------------- multi-GPU */
 /* One process per GPU.  A codeword of 2^log_n is committed by G ranks
@@ -326,6 +371,7 @@ int fri_dist_detach(fri_ctx* ctx);
 #define FRI_TRANSPORT_RCCL 1
 #define FRI_TRANSPORT_HOST 2
 #define FRI_TRANSPORT_LOOPBACK 3   /* fri_debug_attach_loopback (timing rehearsal only) */
+#define FRI_TRANSPORT_PEER     4   /* in-process team (fri_ctx_create_multi): device copies between ranks */
 int fri_dist_info(fri_ctx* ctx, int* rank, int* world, int* transport);
 /* Diagnostic: run the transport's all-to-all, all-gather and pair exchange
  * (both streams) on a known pattern and check the result; FRI_ERCCL with a

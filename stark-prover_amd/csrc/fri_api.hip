@@ -80,14 +80,21 @@ struct Lane {
     DevState* d_state = nullptr;
 };
 
+struct Team;   // in-process team (defined below)
+
 // Collective transport of the sharded commit: RCCL on the context stream, or
-// host-staged callbacks (synchronous; used by the gloo tests).
+// host-staged callbacks (synchronous; used by the gloo tests), or the peer
+// transport of an in-process team (fri_ctx_create_multi: device copies
+// between the ranks' buffers, ordered by events, on the same streams RCCL
+// would use).
 struct Transport {
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;     // main stream collectives
     ncclComm_t xcomm = nullptr;    // exchange stream (separate communicator: no cross-stream ordering hazard)
     bool host = false;
     bool loop = false;          // fri_debug_attach_loopback: every exchange returns this rank's own bytes
+    bool peer = false;          // in-process team, peer transport (peer_op)
+    Team* team = nullptr;       // the team this rank belongs to (peer or team RCCL transport)
     fri_collectives ops{};
     uint8_t* hs = nullptr;      // pinned staging
     uint8_t* hr = nullptr;
@@ -111,6 +118,41 @@ struct DistBuf {
     ShardTop* shtop = nullptr;  // per layer: what the sharded top kernels read (MAXR + 1)
     std::vector<ShardTop> shtop_h;  // the contents last uploaded to shtop (re-uploaded only on change)
     std::vector<int32_t> sched_h;   // loopback rehearsal: recorded degree per layer (fri_debug_loopback_degrees)
+};
+
+// In-process team (fri_ctx_create_multi; see "in-process team" below).
+struct PeerSlot {
+    const void* send;
+    void* recv;
+    size_t bytes;
+    uint32_t op, chan;
+    int peer;
+};
+
+struct Team {
+    uint32_t G = 1, logG = 0;
+    int kind = FRI_TRANSPORT_PEER;          // FRI_TRANSPORT_PEER or FRI_TRANSPORT_RCCL
+    std::vector<int> dev;
+    std::vector<fri_ctx*> rk;               // rk[0] = the owning context
+    bool kernel_pull = true;                // every device can read every other's memory
+    // job dispatch to the worker threads (ranks 1..G-1)
+    std::vector<std::thread> th;
+    std::mutex jm;
+    std::condition_variable jcv, dcv;
+    uint64_t seq = 0;
+    uint32_t left = 0;
+    bool quit = false;
+    std::function<int(uint32_t)> job;
+    std::vector<int> rc;
+    // rendezvous of the peer transport
+    std::mutex bm;
+    std::condition_variable bcv;
+    uint64_t bgen = 0;
+    uint32_t arrived = 0;
+    bool aborted = false;
+    std::string why;
+    std::vector<PeerSlot> slot;
+    std::vector<hipEvent_t> ev_ready, ev_done;   // per rank, created on its device
 };
 
 // One timed launch group: events recorded around it on the context stream.
@@ -153,7 +195,11 @@ struct fri_ctx {
     Plan plan;
     Lane lanes[FRI_MAX_INFLIGHT];   // lanes[cur_lane] is empty: that lane lives in plan / stream / d_state
     int cur_lane = 0;
+    int res_lane = 0;               // lane of the resident commit (init_state): the read-backs serve it
     int max_lanes = FRI_DEFAULT_LANES;
+    int lanes_ok = FRI_MAX_INFLIGHT;   // lanes below this got plan memory (lowered on ENOMEM, pick_lane)
+    int slot_lane[FRI_MAX_INFLIGHT] = {};            // lane of pending slot i
+    uint64_t lane_ticket[FRI_MAX_INFLIGHT] = {};     // last ticket dealt to lane j (0: never)
     bool profiling = false;
     std::map<std::string, ProfEntry> prof;
     std::vector<TimedSpan> spans;      // recorded spans of the current commit
@@ -183,6 +229,7 @@ struct fri_ctx {
     uint32_t* stall_flag_dev = nullptr;
     std::map<const void*, size_t> allocs;   // device allocations owned by the context (fri_ctx_device_bytes)
     size_t dev_bytes = 0, dev_peak = 0;
+    Team* team_root = nullptr;      // fri_ctx_create_multi: this context is rank 0 and owns the team
 };
 
 // Device allocations of a context go through these, so that
@@ -326,6 +373,16 @@ extern "C" int fri_ctx_create(int device, uint32_t log_n_max, fri_ctx** out) {
 }
 
 extern "C" int fri_dist_detach(fri_ctx* ctx);
+// team (fri_ctx_create_multi; defined at the end of this file)
+static void team_destroy(fri_ctx* root);
+static int team_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
+                       uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                       const uint32_t* forced_betas, fri_commit_result* out);
+static int team_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out);
+static int team_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level, uint32_t* w);
+static int team_decommit(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap, uint8_t* paths,
+                         size_t paths_cap, size_t* paths_len);
+static int team_run(fri_ctx* root, const std::function<int(uint32_t)>& fn);
 
 // Free one plan's buffers and graphs (its lane's stream must be idle).
 static void plan_release(fri_ctx* ctx, Plan& p) {
@@ -350,6 +407,7 @@ static void plan_free(fri_ctx* ctx) {
         if (ln.stream) hipStreamSynchronize(ln.stream);
     plan_release(ctx, ctx->plan);
     for (Lane& ln : ctx->lanes) plan_release(ctx, ln.plan);
+    ctx->lanes_ok = FRI_MAX_INFLIGHT;     // memory is back: every lane may build a plan again
 }
 
 // Install lane j in fri_ctx::{plan, stream, d_state} (creating its stream and
@@ -377,6 +435,8 @@ static int use_lane(fri_ctx* ctx, int j) {
 
 extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     if (!ctx) return FRI_EINVAL;
+    if (ctx->tp.team && !ctx->team_root) return fail(ctx, FRI_EINVAL, "a rank of a team: destroy the team's context");
+    if (ctx->team_root) team_destroy(ctx);       // the other ranks, their workers and communicators
     hipSetDevice(ctx->device);
     if (ctx->stuck) {
         // a stream that stayed busy after the RCCL abort: poll it with the
@@ -896,7 +956,9 @@ static int plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, u
         dalloc(ctx, &p.pre_lo, ((size_t)1 << POW_LO_LOG) * 4) != hipSuccess ||
         dalloc(ctx, &p.pre_hi, nhi * 4) != hipSuccess ||
         dalloc(ctx, &p.wgmax, 6 * ((log_n > 8 ? ((size_t)1 << (log_n - 8)) : 1) + 16) * 4) != hipSuccess) {
-        plan_free(ctx);
+        // only the partial plan goes: the other lanes' plans (and lane 0's
+        // input buffer, which fri_ctx_input_buffer handed out) stay valid
+        plan_release(ctx, p);
         return fail(ctx, FRI_ENOMEM, "device allocation failed for commit plan");
     }
     hipStream_t s = ctx->stream;
@@ -1011,6 +1073,7 @@ static void enqueue_commit(fri_ctx* ctx) {
 static void init_state(fri_ctx* ctx, DevState* h, const fri_channel_state* chan_in, uint32_t flags,
                        const uint32_t* forced_betas) {
     ctx->h_state = h;
+    ctx->res_lane = ctx->cur_lane;
     memset(h, 0, sizeof(DevState));      // n_layers = 0: nothing readable until this commit succeeds
     ctx->commit_gen++;
     if (chan_in && chan_in->has_state) {
@@ -1030,8 +1093,13 @@ static void init_state(fri_ctx* ctx, DevState* h, const fri_channel_state* chan_
 }
 
 // Pipelined commits may still be running: a call that reads the resident
-// commit (its pinned state, layers or trees) drains the stream first.
+// commit (its pinned state, layers or trees) drains the stream first.  The
+// resident commit's lane is installed first: a call that switched lanes and
+// then failed before it enqueued anything (a rejected argument, a plan that
+// got no memory) leaves the resident commit on the lane it ran on, so its
+// stream, plan and state are the ones the read-backs must use.
 static void settle(fri_ctx* ctx) {
+    if (ctx->res_lane != ctx->cur_lane) (void)use_lane(ctx, ctx->res_lane);   // (a used lane: cannot fail)
     if (!ctx->async_unsettled) return;
     (void)hipStreamSynchronize(ctx->stream);
     ctx->async_unsettled = false;
@@ -1156,9 +1224,13 @@ static int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t*
                       uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                       const uint32_t* forced_betas, fri_commit_result* out) {
     if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    // (the argument checks before the lane switch; a failure after it leaves
+    // the resident commit on its own lane, see settle)
+    int rc = commit_validate(ctx, d, log_n, offset, flags, forced_betas);
+    if (rc) return rc;
     // synchronous commits run on lane 0, whose input buffer is the one
     // fri_ctx_input_buffer hands out (after any commit pending on that lane)
-    int rc = use_lane(ctx, 0);
+    rc = use_lane(ctx, 0);
     if (rc) return rc;
     rc = commit_enqueue(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, -1);
     if (rc) return rc;
@@ -1172,6 +1244,7 @@ extern "C" int fri_commit(fri_ctx* ctx, const uint32_t* coeffs, size_t d, uint32
                           const fri_channel_state* chan_in, uint32_t flags, const uint32_t* forced_betas,
                           fri_commit_result* out) {
     if (d && !coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    if (ctx && ctx->team_root) return team_commit(ctx, coeffs, nullptr, d, log_n, offset, chan_in, flags, forced_betas, out);
     return run_commit(ctx, coeffs, nullptr, d, log_n, offset, chan_in, flags, forced_betas, out);
 }
 
@@ -1179,6 +1252,8 @@ extern "C" int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t 
                                  uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                                  const uint32_t* forced_betas, fri_commit_result* out) {
     if (d && !d_coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    if (ctx && ctx->team_root)
+        return team_commit(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
     return run_commit(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
 }
 
@@ -1199,6 +1274,28 @@ static hipError_t upload_stream(int device, hipStream_t* out) {
     return e;
 }
 
+// The lane of the next pipelined commit: the one with the fewest pending
+// (un-waited) commits, ties to the lane dealt a ticket longest ago (never
+// used first, lowest index first).  A deal by result slot (slot mod lanes)
+// put two of every four commits on lane 0 at depth 4 over 3 lanes, because
+// the slot a wait frees is reused at once (BENCH_r04: 3.80 ms per commit
+// against 3.32 at depth 3).  Deterministic: no device query.
+static int pick_lane(fri_ctx* ctx) {
+    const int nl = std::max(1, std::min(ctx->max_lanes, ctx->lanes_ok));
+    int best = 0, best_n = FRI_MAX_INFLIGHT + 1;
+    uint64_t best_t = 0;
+    for (int j = 0; j < nl; j++) {
+        int n = 0;
+        for (int i = 0; i < FRI_MAX_INFLIGHT; i++) n += (ctx->slot_pending[i] && ctx->slot_lane[i] == j) ? 1 : 0;
+        if (n < best_n || (n == best_n && ctx->lane_ticket[j] < best_t)) {
+            best = j;
+            best_n = n;
+            best_t = ctx->lane_ticket[j];
+        }
+    }
+    return best;
+}
+
 // Pipelined commits: a free result slot, the commit enqueued with its state
 // in that slot, an event after its copy-out.  Host coefficients are first
 // copied into the slot's pinned buffer, so the caller may reuse its buffer at
@@ -1209,6 +1306,7 @@ static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32
     if (!ctx || !ticket) return fail(ctx, FRI_EINVAL, "null argument");
     if (d && !host_coeffs && !d_coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
     if (ctx->profiling) return fail(ctx, FRI_ESTATE, "profiling: time commits with fri_commit_device");
+    if (ctx->team_root) return fail(ctx, FRI_EINVAL, "multi-GPU context: pipelined commits run on one-device contexts");
     int slot = -1;
     for (int i = 0; i < FRI_MAX_INFLIGHT && slot < 0; i++)
         if (!ctx->slot_pending[i]) slot = i;
@@ -1217,8 +1315,17 @@ static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32
     int rv = commit_validate(ctx, d, log_n, offset, flags, forced_betas);
     if (rv) return rv;
     // this commit's lane (its own stream, plan and device state): the
-    // commits pending on other lanes run beside it
-    if ((rv = use_lane(ctx, slot % ctx->max_lanes))) return rv;
+    // commits pending on other lanes run beside it.  Its plan first: a lane
+    // that gets no memory for it lowers the lanes in use and the commit goes
+    // to one of the others (lane 0 always has one, or the call fails).
+    for (;;) {
+        const int lane = pick_lane(ctx);
+        if ((rv = use_lane(ctx, lane))) return rv;
+        rv = plan_build(ctx, d, log_n, offset);
+        if (rv != FRI_ENOMEM || lane == 0) break;
+        ctx->lanes_ok = lane;
+    }
+    if (rv) return rv;
     // (each lazily created member on its own: one whose creation failed is
     // created on the next call instead of being used null)
     if (!ctx->h_slot[slot]) FRI_HIP(ctx, hipHostMalloc(&ctx->h_slot[slot], sizeof(DevState), hipHostMallocDefault));
@@ -1256,6 +1363,8 @@ static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32
     }
     FRI_HIP(ctx, hipEventRecord(ctx->ev_slot[slot], ctx->stream));
     ctx->slot_pending[slot] = true;
+    ctx->slot_lane[slot] = ctx->cur_lane;
+    ctx->lane_ticket[ctx->cur_lane] = ctx->next_ticket;
     ctx->slot_ticket[slot] = ctx->next_ticket++;
     ctx->slot_log_n[slot] = log_n;
     ctx->async_unsettled = true;
@@ -1295,7 +1404,18 @@ extern "C" int fri_ctx_set_lanes(fri_ctx* ctx, uint32_t max_lanes) {
     for (int i = 0; i < FRI_MAX_INFLIGHT; i++)
         if (ctx->slot_pending[i]) return fail(ctx, FRI_ESTATE, "pipelined commits pending: wait for them first");
     ctx->max_lanes = (int)max_lanes;
+    ctx->lanes_ok = FRI_MAX_INFLIGHT;
     return FRI_OK;
+}
+
+extern "C" int fri_debug_ticket_lane(fri_ctx* ctx, uint64_t ticket, int* lane) {
+    if (!ctx || !lane) return fail(ctx, FRI_EINVAL, "null argument");
+    for (int i = 0; i < FRI_MAX_INFLIGHT; i++)
+        if (ctx->slot_pending[i] && ctx->slot_ticket[i] == ticket) {
+            *lane = ctx->slot_lane[i];
+            return FRI_OK;
+        }
+    return fail(ctx, FRI_EINVAL, "no pending commit with this ticket");
 }
 
 extern "C" int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr) {
@@ -1315,7 +1435,7 @@ extern "C" int fri_commit_info(fri_ctx* ctx, uint64_t* generation, uint32_t* log
     if (!ctx || !generation || !log_n || !n_layers) return fail(ctx, FRI_EINVAL, "null argument");
     settle(ctx);
     *generation = ctx->commit_gen;
-    *n_layers = ctx->h_state->n_layers;
+    *n_layers = ctx->plan.valid ? ctx->h_state->n_layers : 0u;   // (a plan change frees the layers)
     *log_n = *n_layers ? ctx->commit_log_n : 0u;
     return FRI_OK;
 }
@@ -1325,10 +1445,11 @@ extern "C" int fri_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out, size_
     settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
-    if (layer < ctx->sharded_layers)
+    if (layer < ctx->sharded_layers && !ctx->team_root)
         return fail(ctx, FRI_ESTATE, "layer was committed sharded: this rank holds only its block (fri_commit_sharded)");
     size_t m = (size_t)1 << (p.log_n - layer);
     if (cap < m) return fail(ctx, FRI_EINVAL, "output buffer too small");
+    if (layer < ctx->sharded_layers) return team_layer_copy(ctx, layer, out);     // the ranks' blocks
     // on the context stream: the null stream would hold a hardware queue of
     // its own (GPU_MAX_HW_QUEUES) for the rest of the process, one fewer for
     // the commit lanes and other contexts
@@ -1342,16 +1463,21 @@ extern "C" int fri_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level,
     settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
-    if (layer < ctx->sharded_layers)
+    if (layer < ctx->sharded_layers && !ctx->team_root)
         return fail(ctx, FRI_ESTATE, "layer was committed sharded: this rank holds only its block (fri_commit_sharded)");
     uint32_t L = p.log_n - layer;
     if (level > L) return fail(ctx, FRI_EINVAL, "level above root");
     size_t cnt = (size_t)1 << (L - level);
     if (cap < cnt * 32) return fail(ctx, FRI_EINVAL, "output buffer too small");
     std::vector<uint32_t> w(cnt * 8);
-    FRI_HIP(ctx, hipMemcpyAsync(w.data(), p.trees + p.tree_off[layer] + 8 * level_offset(L, level), cnt * 32,
-                                hipMemcpyDeviceToHost, ctx->stream));   // (not the null stream: fri_layer_copy)
-    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (layer < ctx->sharded_layers) {
+        const int rc = team_tree_level_copy(ctx, layer, level, w.data());    // block trees + top tree
+        if (rc) return rc;
+    } else {
+        FRI_HIP(ctx, hipMemcpyAsync(w.data(), p.trees + p.tree_off[layer] + 8 * level_offset(L, level), cnt * 32,
+                                    hipMemcpyDeviceToHost, ctx->stream));   // (not the null stream: fri_layer_copy)
+        FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     for (size_t i = 0; i < cnt; i++) digest_to_bytes(&w[8 * i], out + 32 * i);
     return FRI_OK;
 }
@@ -1368,10 +1494,29 @@ extern "C" int fri_auth_path(fri_ctx* ctx, uint32_t layer, uint64_t index, uint3
     settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || layer >= ctx->h_state->n_layers) return fail(ctx, FRI_ESTATE, "no such committed layer");
-    if (layer < ctx->sharded_layers)
+    if (layer < ctx->sharded_layers && !ctx->team_root)
         return fail(ctx, FRI_ESTATE, "layer was committed sharded: this rank holds only its block (fri_commit_sharded)");
     uint32_t L = p.log_n - layer;
     if (index >> L) return fail(ctx, FRI_EINVAL, "index out of range");
+    if (layer < ctx->sharded_layers) {
+        // a team commit: the decommitment of `index` (idx_k = index mod m_k =
+        // index for this layer) through the ranks, then this layer's part
+        const uint32_t nl = ctx->h_state->n_layers;
+        size_t total = 0, off = 0;
+        for (uint32_t k = 0; k < nl; k++) {
+            if (k == layer) off = total;
+            total += (size_t)64 * (p.log_n - k);
+        }
+        std::vector<uint32_t> vals(2 * (size_t)nl);
+        std::vector<uint8_t> pb(total);
+        size_t plen = 0;
+        const int rc = team_decommit(ctx, index, vals.data(), vals.size(), pb.data(), pb.size(), &plen);
+        if (rc) return rc;
+        *value_out = vals[2 * layer];
+        if (path) memcpy(path, pb.data() + off, (size_t)32 * L);
+        *depth_out = L;
+        return FRI_OK;
+    }
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     int rc = dq_alloc(ctx);
     if (rc) return rc;
@@ -1410,6 +1555,8 @@ extern "C" int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values
     settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || ctx->h_state->n_layers == 0) return fail(ctx, FRI_ESTATE, "no committed layers");
+    if (ctx->sharded_layers && ctx->team_root)
+        return team_decommit(ctx, index, values, values_cap, paths, paths_cap, paths_len);
     if (ctx->sharded_layers)
         return fail(ctx, FRI_ESTATE, "last commit was sharded: each rank holds only its blocks of the large layers");
     DecommitPlan dp{};
@@ -1626,6 +1773,11 @@ extern "C" int fri_ctx_device_bytes(fri_ctx* ctx, uint64_t* current, uint64_t* p
     if (!ctx || !current || !peak) return fail(ctx, FRI_EINVAL, "null argument");
     *current = ctx->dev_bytes;
     *peak = ctx->dev_peak;
+    if (ctx->team_root)                        // a team: every rank's (fri_debug_team_rank for one)
+        for (uint32_t r = 1; r < ctx->team_root->G; r++) {
+            *current += ctx->team_root->rk[r]->dev_bytes;
+            *peak += ctx->team_root->rk[r]->dev_peak;
+        }
     return FRI_OK;
 }
 
@@ -1710,6 +1862,115 @@ static int sync_sharded(fri_ctx* ctx, hipStream_t s) {
                                     (drained ? ")" : "; stream still busy: destroy the context)"));
 }
 
+// ------------------------------------------------ in-process team ----
+// fri_ctx_create_multi: one context per device (rank r drives devices[r]),
+// rank 0 being the context handed to the caller.  A team call (fri_commit,
+// fri_decommit_query, ...) runs the coset-sharded protocol of
+// run_commit_sharded on every rank at once: rank 0 on the calling thread,
+// ranks 1..G-1 on persistent worker threads of the team (one per rank, so a
+// rank's HIP calls stay on its own thread and device).  The collectives go
+// over RCCL (communicators from ncclCommInitAll) or over the peer transport:
+//   each collective, on rank r:  record ready_r after its producer on the
+//   op's stream; post (op, bytes, peer, send, recv); rendezvous A; check that
+//   every rank posted the same (op, bytes) and matched peers (the
+//   deadlock-freedom condition of DESIGN.md §7, enforced here rather than
+//   only logged); the stream waits for the sources' ready events and one
+//   k_peer_pull reads every source's bytes (same device, or another device
+//   over xGMI through peer access); record done_r; rendezvous B; the stream
+//   waits for the done events of the ranks that read r's send buffer.
+// Every event waited on was recorded before the rendezvous that precedes the
+// wait, so no stream can wait for work that has not been submitted (no
+// deadlock, even when ranks share a device and its hardware queues), and a
+// rank that fails aborts the rendezvous: the others return FRI_ERCCL
+// instead of blocking.  The GPU never waits for the host.
+static void team_abort(Team* T, const std::string& why) {
+    std::lock_guard<std::mutex> g(T->bm);
+    if (!T->aborted) T->why = why;
+    T->aborted = true;
+    T->bcv.notify_all();
+}
+
+// All G ranks arrive; false when the team was aborted first.
+static bool team_barrier(Team* T) {
+    std::unique_lock<std::mutex> lk(T->bm);
+    if (T->aborted) return false;
+    const uint64_t g = T->bgen;
+    if (++T->arrived == T->G) {
+        T->arrived = 0;
+        T->bgen++;
+        T->bcv.notify_all();
+        return true;
+    }
+    T->bcv.wait(lk, [&] { return T->bgen != g || T->aborted; });
+    return T->bgen != g;
+}
+
+static const char* op_name(uint32_t op) {
+    return op == FRI_OP_ALLGATHER ? "allgather" : op == FRI_OP_ALLTOALL ? "alltoall" : "sendrecv";
+}
+
+// One collective of the peer transport (see Team).  ALLTOALL: recv[p] =
+// p's send[r]; ALLGATHER: recv[p] = p's send; SENDRECV: recv = peer's send.
+static int peer_op(fri_ctx* ctx, uint32_t op, uint32_t chan, const void* send, void* recv, size_t bytes, int peer,
+                   hipStream_t s) {
+    Team* T = ctx->tp.team;
+    const uint32_t r = (uint32_t)ctx->tp.rank, G = T->G;
+    if (bytes % 4) return fail(ctx, FRI_EINVAL, "peer transport: byte count not a multiple of 4");
+    FRI_HIP(ctx, hipEventRecord(T->ev_ready[r], s));
+    T->slot[r] = PeerSlot{send, recv, bytes, op, chan, peer};
+    if (!team_barrier(T)) return fail(ctx, FRI_ERCCL, "peer transport: another rank failed (" + T->why + ")");
+    for (uint32_t p = 0; p < G; p++) {
+        const PeerSlot& q = T->slot[p];
+        if (q.op != op || q.bytes != bytes || q.chan != chan ||
+            (op == FRI_OP_SENDRECV && (q.peer < 0 || q.peer >= (int)G || T->slot[q.peer].peer != (int)p))) {
+            const std::string m = std::string("peer transport: schedule mismatch at ") + op_name(op) + " (rank " +
+                                  std::to_string(p) + " posted " + op_name(q.op) + " of " + std::to_string(q.bytes) +
+                                  " bytes)";
+            team_abort(T, m);
+            return fail(ctx, FRI_ERCCL, m);
+        }
+    }
+    // (the slots are stable from rendezvous A to B: a rank posts its next op
+    // only after B, which waits for this one; so everything read from them is
+    // read here)
+    std::vector<uint32_t> readers;        // ranks that read this rank's send buffer
+    for (uint32_t p = 0; p < G; p++)
+        if (p != r && (op != FRI_OP_SENDRECV || T->slot[p].peer == (int)r)) readers.push_back(p);
+    PeerPull pp{};
+    pp.dst = static_cast<uint32_t*>(recv);
+    pp.words = bytes / 4;
+    std::vector<uint32_t> srcs;
+    if (op == FRI_OP_SENDRECV) {
+        srcs.push_back((uint32_t)peer);
+    } else {
+        for (uint32_t p = 0; p < G; p++) srcs.push_back(p);
+    }
+    bool vec4 = pp.words % 4 == 0 && (reinterpret_cast<uintptr_t>(recv) & 15) == 0;
+    for (size_t i = 0; i < srcs.size(); i++) {
+        const uint32_t p = srcs[i];
+        const uint8_t* base = static_cast<const uint8_t*>(T->slot[p].send) + (op == FRI_OP_ALLTOALL ? (size_t)r * bytes : 0);
+        pp.src[i] = reinterpret_cast<const uint32_t*>(base);
+        vec4 = vec4 && (reinterpret_cast<uintptr_t>(base) & 15) == 0;
+        if (p != r) FRI_HIP(ctx, hipStreamWaitEvent(s, T->ev_ready[p], 0));
+    }
+    pp.n = (uint32_t)srcs.size();
+    pp.vec4 = vec4 ? 1u : 0u;
+    if (T->kernel_pull) {
+        launch_peer_pull(pp, s);
+        FRI_HIP(ctx, hipGetLastError());
+    } else {
+        for (uint32_t i = 0; i < pp.n; i++) {
+            const uint32_t p = srcs[i];
+            FRI_HIP(ctx, hipMemcpyPeerAsync(pp.dst + (size_t)i * pp.words, T->dev[r], pp.src[i], T->dev[p], bytes, s));
+        }
+    }
+    FRI_HIP(ctx, hipEventRecord(T->ev_done[r], s));
+    if (!team_barrier(T)) return fail(ctx, FRI_ERCCL, "peer transport: another rank failed (" + T->why + ")");
+    // this rank's send buffer may be rewritten only after its readers' pulls
+    for (uint32_t p : readers) FRI_HIP(ctx, hipStreamWaitEvent(s, T->ev_done[p], 0));
+    return FRI_OK;
+}
+
 // Every transport call is logged (fri_debug_transport_log): chan 0 is the main
 // communicator on the context stream, 1 the exchange communicator on the
 // exchange stream, whatever stream the host transport actually uses.
@@ -1725,6 +1986,7 @@ static void tp_log(fri_ctx* ctx, uint32_t chan, uint32_t op, int peer, size_t by
 static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
     Transport& tp = ctx->tp;
     tp_log(ctx, 0, FRI_OP_ALLGATHER, -1, bytes);
+    if (tp.peer) return peer_op(ctx, FRI_OP_ALLGATHER, 0, dsend, drecv, bytes, -1, s);
     if (tp.loop) {                     // G copies of this rank's bytes, one launch (bytes: whole words)
         launch_replicate(static_cast<const uint32_t*>(dsend), static_cast<uint32_t*>(drecv), bytes / 4,
                          (uint32_t)tp.world, s);
@@ -1747,6 +2009,7 @@ static int tp_allgather(fri_ctx* ctx, const void* dsend, void* drecv, size_t byt
 static int tp_alltoall(fri_ctx* ctx, const void* dsend, void* drecv, size_t bytes_per_peer, hipStream_t s) {
     Transport& tp = ctx->tp;
     tp_log(ctx, 0, FRI_OP_ALLTOALL, -1, bytes_per_peer);
+    if (tp.peer) return peer_op(ctx, FRI_OP_ALLTOALL, 0, dsend, drecv, bytes_per_peer, -1, s);
     if (tp.loop) {
         FRI_HIP(ctx, hipMemcpyAsync(drecv, dsend, bytes_per_peer * tp.world, hipMemcpyDeviceToDevice, s));
         return FRI_OK;
@@ -1783,6 +2046,7 @@ static int tp_sendrecv(fri_ctx* ctx, const void* dsend, void* drecv, size_t byte
                        uint32_t chan) {
     Transport& tp = ctx->tp;
     tp_log(ctx, chan, FRI_OP_SENDRECV, peer, bytes);
+    if (tp.peer) return peer_op(ctx, FRI_OP_SENDRECV, chan, dsend, drecv, bytes, peer, s);
     if (tp.loop) {
         FRI_HIP(ctx, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, s));
         return FRI_OK;
@@ -1818,7 +2082,12 @@ static int dist_check(fri_ctx* ctx, int rank, int world) {
     return FRI_OK;
 }
 
+static int team_guard(fri_ctx* ctx) {
+    return ctx && ctx->tp.team ? fail(ctx, FRI_EINVAL, "multi-GPU context: its transport is the team's") : FRI_OK;
+}
+
 extern "C" int fri_dist_attach_rccl(fri_ctx* ctx, int rank, int world, const uint8_t uid[128]) {
+    if (int g = team_guard(ctx)) return g;
     int rc = dist_check(ctx, rank, world);
     if (rc) return rc;
     if (!uid) return fail(ctx, FRI_EINVAL, "null unique id");
@@ -1877,6 +2146,7 @@ extern "C" int fri_dist_attach_rccl(fri_ctx* ctx, int rank, int world, const uin
 }
 
 extern "C" int fri_dist_attach_host(fri_ctx* ctx, int rank, int world, const fri_collectives* ops) {
+    if (int g = team_guard(ctx)) return g;
     int rc = dist_check(ctx, rank, world);
     if (rc) return rc;
     if (!ops || !ops->allgather || !ops->alltoall || !ops->sendrecv) return fail(ctx, FRI_EINVAL, "null callback");
@@ -1893,6 +2163,7 @@ extern "C" int fri_dist_attach_host(fri_ctx* ctx, int rank, int world, const fri
 // the calling stream (the exchange stream included, as with RCCL), so the
 // GPU never waits for a host round trip.  The transcript is not the real one.
 extern "C" int fri_debug_attach_loopback(fri_ctx* ctx, int rank, int world) {
+    if (int g = team_guard(ctx)) return g;
     int rc = dist_check(ctx, rank, world);
     if (rc) return rc;
     fri_dist_detach(ctx);
@@ -1931,6 +2202,7 @@ extern "C" int fri_debug_transport_log(fri_ctx* ctx, fri_transport_op* out, size
 
 extern "C" int fri_dist_detach(fri_ctx* ctx) {
     if (!ctx) return FRI_EINVAL;
+    if (int g = team_guard(ctx)) return g;
     Transport& tp = ctx->tp;
     if (tp.xcomm) ncclCommDestroy(tp.xcomm);
     if (tp.comm) ncclCommDestroy(tp.comm);
@@ -1944,8 +2216,8 @@ extern "C" int fri_dist_detach(fri_ctx* ctx) {
 extern "C" int fri_dist_info(fri_ctx* ctx, int* rank, int* world, int* transport) {
     if (!ctx || !rank || !world || !transport) return fail(ctx, FRI_EINVAL, "null argument");
     const Transport& tp = ctx->tp;
-    if (tp.host || tp.loop) {
-        *transport = tp.host ? FRI_TRANSPORT_HOST : FRI_TRANSPORT_LOOPBACK;
+    if (tp.host || tp.loop || tp.peer) {
+        *transport = tp.host ? FRI_TRANSPORT_HOST : tp.loop ? FRI_TRANSPORT_LOOPBACK : FRI_TRANSPORT_PEER;
         *rank = tp.rank;
         *world = tp.world;
     } else if (tp.comm) {
@@ -1967,9 +2239,19 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords);
 // streams/communicators, checked on the host.  Rank r sends word
 // (r << 24) | (p << 16) | i to peer p; the exchange partner is r ^ 1 (itself
 // when world == 1).
+static int dist_selftest(fri_ctx* ctx, size_t words_per_peer);
 extern "C" int fri_dist_selftest(fri_ctx* ctx, size_t words_per_peer) {
     if (!ctx) return FRI_EINVAL;
-    if (ctx->tp.world < 1 || (!ctx->tp.host && !ctx->tp.comm)) return fail(ctx, FRI_ESTATE, "no transport attached");
+    if (ctx->team_root) {
+        Team* T = ctx->team_root;
+        return team_run(ctx, [&](uint32_t r) { return dist_selftest(T->rk[r], words_per_peer); });
+    }
+    return dist_selftest(ctx, words_per_peer);
+}
+
+static int dist_selftest(fri_ctx* ctx, size_t words_per_peer) {
+    if (ctx->tp.world < 1 || (!ctx->tp.host && !ctx->tp.comm && !ctx->tp.peer))
+        return fail(ctx, FRI_ESTATE, "no transport attached");
     const uint32_t G = (uint32_t)ctx->tp.world, r = (uint32_t)ctx->tp.rank;
     if (words_per_peer == 0 || words_per_peer > ((size_t)1 << 16)) return fail(ctx, FRI_EINVAL, "1 <= words_per_peer <= 65536");
     const size_t W = words_per_peer, tot = W * G;
@@ -2059,7 +2341,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     while ((1u << logG) < G) logG++;
     if (G == 1 || log_n < SHARD_MIN_LOG || log_n < logG + 12)
         return run_commit(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
-    if (!ctx->tp.host && !ctx->tp.comm && !ctx->tp.loop) return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
+    if (!ctx->tp.host && !ctx->tp.comm && !ctx->tp.loop && !ctx->tp.peer)
+        return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
     // a rank holds 1/G of the codeword: its NTT, twiddles and scratch are block-sized
     if (log_n - logG > ctx->log_n_max) return fail(ctx, FRI_EINVAL, "log_n - log2(world) out of range for context");
     const size_t n = (size_t)1 << log_n;
@@ -2085,8 +2368,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
     if (host_coeffs && d)
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
-    else if (dev_coeffs && dev_coeffs != p.d_in && d)
-        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, s));
+    else if (dev_coeffs && dev_coeffs != p.d_in && d)   // (Default: a team rank reads rank 0's device buffer)
+        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDefault, s));
 
     size_t sp;
     if (G == 2) {
@@ -2228,15 +2511,21 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         // this rank's record (block root, the maxima of the coefficient
         // slice, the slice's first coefficient) for the all-gather.
         if (!side) launch_coef(tc, Gc, s);
+        // (the ordering calls' errors are returned: without the wait the
+        // coefficient task is not ordered after the leaf kernel, without the
+        // record the block top's wait binds to an older one and reads stale maxima)
+        hipError_t beside_err = hipSuccess;
         auto coef_beside = [&]() {
-            (void)hipStreamWaitEvent(ctx->cstream, ctx->ev_pre, 0);
+            beside_err = hipStreamWaitEvent(ctx->cstream, ctx->ev_pre, 0);
+            if (beside_err != hipSuccess) return;
             launch_coef(tc, Gc, ctx->cstream);
-            (void)hipEventRecord(ctx->ev_coef, ctx->cstream);
+            beside_err = hipEventRecord(ctx->ev_coef, ctx->cstream);
         };
         tl.shard = db.shtop + k;
         launch_layer(tl, s, side ? ctx->ev_pre : (spl == (size_t)-1 ? nullptr : ctx->spans[spl].e),
                      side ? std::function<void()>(coef_beside) : std::function<void()>(),
                      side ? ctx->ev_coef : nullptr);
+        FRI_HIP(ctx, beside_err);
         FRI_HIP(ctx, hipGetLastError());
         // all ranks' records; the replicated top reads the block roots (in
         // block order), the maxima and rank 0's first coefficient from them
@@ -2339,14 +2628,29 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
 // replicated local layers are equal everywhere).  Collective: every rank
 // calls it with the same index and gets the same bytes, which equal
 // fri_decommit_query's for a 1-GPU commit of the same codeword.
+static int decommit_sharded(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap, uint8_t* paths,
+                            size_t paths_cap, size_t* paths_len);
+
 extern "C" int fri_decommit_query_sharded(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap,
                                           uint8_t* paths, size_t paths_cap, size_t* paths_len) {
+    if (!ctx || !values || !paths_len) return fail(ctx, FRI_EINVAL, "null argument");
+    if (ctx->team_root) {
+        settle(ctx);
+        if (!ctx->sharded_layers) return fail(ctx, FRI_ESTATE, "last commit was not sharded: use fri_decommit_query");
+        return team_decommit(ctx, index, values, values_cap, paths, paths_cap, paths_len);
+    }
+    return decommit_sharded(ctx, index, values, values_cap, paths, paths_cap, paths_len);
+}
+
+static int decommit_sharded(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap, uint8_t* paths,
+                            size_t paths_cap, size_t* paths_len) {
     if (!ctx || !values || !paths_len) return fail(ctx, FRI_EINVAL, "null argument");
     settle(ctx);
     const Plan& p = ctx->plan;
     if (!p.valid || ctx->h_state->n_layers == 0) return fail(ctx, FRI_ESTATE, "no committed layers");
     if (!ctx->sharded_layers || !p.sharded) return fail(ctx, FRI_ESTATE, "last commit was not sharded: use fri_decommit_query");
-    if (!ctx->tp.host && !ctx->tp.comm && !ctx->tp.loop) return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
+    if (!ctx->tp.host && !ctx->tp.comm && !ctx->tp.loop && !ctx->tp.peer)
+        return fail(ctx, FRI_ESTATE, "no transport attached (detached or aborted)");
     const uint32_t G = p.G;
     if ((uint32_t)ctx->tp.world != G) return fail(ctx, FRI_ESTATE, "transport world differs from the commit's");
     uint32_t logG = 0;
@@ -2401,6 +2705,7 @@ extern "C" int fri_commit_sharded(fri_ctx* ctx, const uint32_t* coeffs, size_t d
                                   const fri_channel_state* chan_in, uint32_t flags, const uint32_t* forced_betas,
                                   fri_commit_result* out) {
     if (d && !coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    if (ctx && ctx->team_root) return team_commit(ctx, coeffs, nullptr, d, log_n, offset, chan_in, flags, forced_betas, out);
     return run_commit_sharded(ctx, coeffs, nullptr, d, log_n, offset, chan_in, flags, forced_betas, out);
 }
 
@@ -2408,5 +2713,319 @@ extern "C" int fri_commit_sharded_device(fri_ctx* ctx, const uint32_t* d_coeffs,
                                          uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                                          const uint32_t* forced_betas, fri_commit_result* out) {
     if (d && !d_coeffs) return fail(ctx, FRI_EINVAL, "null coefficients");
+    if (ctx && ctx->team_root)
+        return team_commit(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
     return run_commit_sharded(ctx, nullptr, d_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
+}
+
+// =========================================================== team (multi-GPU)
+// Run fn(r) on every rank of the team at once: rank 0 on this thread, the
+// others on the team's workers.  The first failing rank aborts the
+// rendezvous (the others' collectives then fail instead of blocking); its
+// message becomes the context's error.
+static void team_worker(Team* T, uint32_t r) {
+    uint64_t seen = 0;
+    for (;;) {
+        std::function<int(uint32_t)> fn;
+        {
+            std::unique_lock<std::mutex> lk(T->jm);
+            T->jcv.wait(lk, [&] { return T->quit || T->seq != seen; });
+            if (T->quit) return;
+            seen = T->seq;
+            fn = T->job;
+        }
+        (void)hipSetDevice(T->dev[r]);
+        const int rc = fn(r);
+        if (rc) team_abort(T, "rank " + std::to_string(r) + ": " + T->rk[r]->err);
+        std::lock_guard<std::mutex> g(T->jm);
+        T->rc[r] = rc;
+        if (--T->left == 0) T->dcv.notify_all();
+    }
+}
+
+static int team_run(fri_ctx* root, const std::function<int(uint32_t)>& fn) {
+    Team* T = root->team_root;
+    {
+        std::lock_guard<std::mutex> g(T->bm);
+        T->aborted = false;
+        T->arrived = 0;
+        T->why.clear();
+    }
+    {
+        std::lock_guard<std::mutex> g(T->jm);
+        T->job = fn;
+        T->left = T->G - 1;
+        std::fill(T->rc.begin(), T->rc.end(), 0);
+        T->seq++;
+    }
+    T->jcv.notify_all();
+    const int rc0 = fn(0);
+    if (rc0) team_abort(T, "rank 0: " + root->err);
+    {
+        std::unique_lock<std::mutex> lk(T->jm);
+        T->dcv.wait(lk, [&] { return T->left == 0; });
+    }
+    int rc = rc0;
+    for (uint32_t r = 1; r < T->G && !rc; r++) rc = T->rc[r];
+    if (rc) {
+        // the failure that aborted the team, and every rank's streams drained
+        // (a rank that returned early may have left work queued)
+        {
+            std::lock_guard<std::mutex> g(T->bm);
+            root->err = T->why.empty() ? root->err : T->why;
+        }
+        for (fri_ctx* c : T->rk) {
+            (void)hipSetDevice(c->device);
+            if (c->stuck) continue;
+            for (hipStream_t st : {c->stream, c->xstream, c->cstream})
+                if (st) (void)hipStreamSynchronize(st);
+        }
+        (void)hipSetDevice(root->device);
+    }
+    return rc;
+}
+
+static void team_free(Team* T) {
+    {
+        std::lock_guard<std::mutex> g(T->jm);
+        T->quit = true;
+    }
+    T->jcv.notify_all();
+    for (auto& t : T->th)
+        if (t.joinable()) t.join();
+    for (uint32_t r = 0; r < T->G; r++) {
+        if (r < T->ev_ready.size() && T->ev_ready[r]) { (void)hipSetDevice(T->dev[r]); hipEventDestroy(T->ev_ready[r]); }
+        if (r < T->ev_done.size() && T->ev_done[r]) { (void)hipSetDevice(T->dev[r]); hipEventDestroy(T->ev_done[r]); }
+    }
+    delete T;
+}
+
+extern "C" int fri_ctx_create_multi(const int* devices, uint32_t n, uint32_t log_n_max, int transport, fri_ctx** out) {
+    if (!out) return FRI_EINVAL;
+    *out = nullptr;
+    if (n < 1 || n > 64 || (n & (n - 1)) || log_n_max < 1 || log_n_max > 30) return FRI_EINVAL;
+    if (transport != FRI_TRANSPORT_NONE && transport != FRI_TRANSPORT_RCCL && transport != FRI_TRANSPORT_PEER)
+        return FRI_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return FRI_ENODEV;
+    std::vector<int> dev(n);
+    for (uint32_t r = 0; r < n; r++) {
+        dev[r] = devices ? devices[r] : (int)r;
+        if (dev[r] < 0 || dev[r] >= ndev) return FRI_ENODEV;
+    }
+    if (n == 1) return fri_ctx_create(dev[0], log_n_max, out);
+    uint32_t logG = 0;
+    while ((1u << logG) < n) logG++;
+    // rank contexts are shard-sized; rank 0 also commits < 2^20 codewords alone
+    const uint32_t sub = std::max(log_n_max > logG ? log_n_max - logG : 1u, std::min(log_n_max, SHARD_MIN_LOG - 1));
+    Team* T = new Team();
+    T->G = n;
+    T->logG = logG;
+    T->dev = dev;
+    T->rk.assign(n, nullptr);
+    T->rc.assign(n, 0);
+    T->slot.assign(n, PeerSlot{});
+    T->ev_ready.assign(n, nullptr);
+    T->ev_done.assign(n, nullptr);
+    int rc = FRI_OK;
+    auto undo = [&](int code) {
+        for (uint32_t r = 1; r < n; r++)
+            if (T->rk[r]) { T->rk[r]->tp = Transport(); fri_ctx_destroy(T->rk[r]); }
+        if (T->rk[0]) { T->rk[0]->tp = Transport(); T->rk[0]->team_root = nullptr; fri_ctx_destroy(T->rk[0]); }
+        team_free(T);
+        return code;
+    };
+    for (uint32_t r = 0; r < n; r++)
+        if ((rc = fri_ctx_create(dev[r], sub, &T->rk[r]))) return undo(rc);
+    for (uint32_t r = 0; r < n; r++) {
+        if (hipSetDevice(dev[r]) != hipSuccess ||
+            hipEventCreateWithFlags(&T->ev_ready[r], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&T->ev_done[r], hipEventDisableTiming) != hipSuccess)
+            return undo(FRI_EHIP);
+    }
+    // peer access between distinct devices: the pull kernel reads the other
+    // ranks' buffers over xGMI; without it, per-source hipMemcpyPeerAsync
+    for (uint32_t a = 0; a < n; a++)
+        for (uint32_t b = 0; b < n; b++) {
+            if (dev[a] == dev[b]) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, dev[a], dev[b]) != hipSuccess || !can) { T->kernel_pull = false; continue; }
+            (void)hipSetDevice(dev[a]);
+            const hipError_t e = hipDeviceEnablePeerAccess(dev[b], 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) T->kernel_pull = false;
+            (void)hipGetLastError();
+        }
+    // transport: RCCL (one communicator per rank for the main stream, one for
+    // the exchange stream) when asked or when automatic and it initialises;
+    // ranks sharing a device can only use the peer transport
+    bool distinct = true;
+    for (uint32_t a = 0; a < n; a++)
+        for (uint32_t b = a + 1; b < n; b++) distinct = distinct && dev[a] != dev[b];
+    T->kind = FRI_TRANSPORT_PEER;
+    if (transport != FRI_TRANSPORT_PEER && distinct) {
+        std::vector<ncclComm_t> c(n, nullptr), x(n, nullptr);
+        ncclResult_t nr = ncclCommInitAll(c.data(), (int)n, dev.data());
+        if (nr == ncclSuccess) {
+            nr = ncclCommInitAll(x.data(), (int)n, dev.data());
+            if (nr != ncclSuccess)
+                for (auto cm : c) ncclCommDestroy(cm);
+        }
+        if (nr == ncclSuccess) {
+            T->kind = FRI_TRANSPORT_RCCL;
+            for (uint32_t r = 0; r < n; r++) { T->rk[r]->tp.comm = c[r]; T->rk[r]->tp.xcomm = x[r]; }
+        } else if (transport == FRI_TRANSPORT_RCCL) {
+            T->rk[0]->err = std::string("ncclCommInitAll: ") + ncclGetErrorString(nr);
+            return undo(FRI_ERCCL);
+        }
+    } else if (transport == FRI_TRANSPORT_RCCL) {
+        return undo(FRI_EINVAL);                 // ranks share a device: RCCL cannot run them
+    }
+    for (uint32_t r = 0; r < n; r++) {
+        Transport& tp = T->rk[r]->tp;
+        tp.rank = (int)r;
+        tp.world = (int)n;
+        tp.team = T;
+        tp.peer = T->kind == FRI_TRANSPORT_PEER;
+    }
+    try {
+        for (uint32_t r = 1; r < n; r++) T->th.emplace_back(team_worker, T, r);
+    } catch (...) {
+        return undo(FRI_ENOMEM);
+    }
+    T->rk[0]->team_root = T;
+    (void)hipSetDevice(dev[0]);
+    *out = T->rk[0];
+    return FRI_OK;
+}
+
+extern "C" int fri_debug_team_rank(fri_ctx* ctx, uint32_t rank, fri_ctx** out) {
+    if (!ctx || !out) return fail(ctx, FRI_EINVAL, "null argument");
+    if (!ctx->team_root) {
+        if (rank) return fail(ctx, FRI_EINVAL, "not a multi-GPU context: rank 0 only");
+        *out = ctx;
+        return FRI_OK;
+    }
+    if (rank >= ctx->team_root->G) return fail(ctx, FRI_EINVAL, "rank out of range");
+    *out = ctx->team_root->rk[rank];
+    return FRI_OK;
+}
+
+// Destroy the ranks of a team (called by fri_ctx_destroy on rank 0 before
+// rank 0's own teardown): each rank detaches on its own thread (RCCL
+// communicators of one clique are destroyed together), then the workers end.
+static void team_destroy(fri_ctx* root) {
+    Team* T = root->team_root;
+    (void)team_run(root, [T](uint32_t r) {
+        fri_ctx* c = T->rk[r];
+        if (c->tp.xcomm) ncclCommDestroy(c->tp.xcomm);
+        if (c->tp.comm) ncclCommDestroy(c->tp.comm);
+        c->tp.comm = c->tp.xcomm = nullptr;
+        return FRI_OK;
+    });
+    for (uint32_t r = 1; r < T->G; r++) {
+        T->rk[r]->tp.team = nullptr;
+        fri_ctx_destroy(T->rk[r]);
+    }
+    root->tp.team = nullptr;
+    root->team_root = nullptr;
+    team_free(T);
+    (void)hipSetDevice(root->device);
+}
+
+// Codewords the team commits sharded (run_commit_sharded's own threshold);
+// smaller ones run on rank 0 alone.
+static bool team_shards(const Team* T, uint32_t log_n) {
+    return log_n >= SHARD_MIN_LOG && log_n >= T->logG + 12;
+}
+
+static int team_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
+                       uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
+                       const uint32_t* forced_betas, fri_commit_result* out) {
+    Team* T = ctx->team_root;
+    if (!out) return fail(ctx, FRI_EINVAL, "null argument");
+    if (!team_shards(T, log_n))
+        return run_commit(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
+    std::vector<fri_commit_result> res(T->G);
+    int rc = team_run(ctx, [&](uint32_t r) {
+        return run_commit_sharded(T->rk[r], host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas,
+                                  &res[r]);
+    });
+    if (rc) return rc;
+    // the redundant tops give every rank the whole transcript: they must agree
+    for (uint32_t r = 1; r < T->G; r++)
+        if (memcmp(&res[r], &res[0], sizeof(fri_commit_result)))
+            return fail(ctx, FRI_ERCCL, "team ranks disagree on the transcript (rank " + std::to_string(r) + ")");
+    *out = res[0];
+    ctx->err.clear();
+    return FRI_OK;
+}
+
+// Sharded layer k of the resident team commit, read back whole: rank r holds
+// block p.block[k] of it (the switch layer's slot, gathered when the tail
+// went local, holds the whole layer on every rank and is read from rank 0).
+static int team_layer_copy(fri_ctx* ctx, uint32_t layer, uint32_t* out) {
+    Team* T = ctx->team_root;
+    const Plan& p0 = ctx->plan;
+    const uint32_t L = p0.log_n - layer;
+    const bool whole = (int)layer == p0.k_sw && p0.k_sw < p0.rmax;
+    const size_t B = (size_t)1 << (L - T->logG);
+    for (uint32_t r = 0; r < (whole ? 1u : T->G); r++) {
+        fri_ctx* c = T->rk[r];
+        const Plan& p = c->plan;
+        FRI_HIP(ctx, hipSetDevice(c->device));
+        const size_t words = whole ? ((size_t)1 << L) : B;
+        FRI_HIP(ctx, hipMemcpyAsync(out + (whole ? 0 : (size_t)p.block[layer] * B), p.layers + p.layer_off[layer],
+                                    words * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    for (uint32_t r = 0; r < (whole ? 1u : T->G); r++) FRI_HIP(ctx, hipStreamSynchronize(T->rk[r]->stream));
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    return FRI_OK;
+}
+
+// Level `level` of sharded layer k's tree: the lower L - log G levels from
+// the ranks' block trees (block order), the top log G levels from the top
+// tree every rank built (rank 0's).
+static int team_tree_level_copy(fri_ctx* ctx, uint32_t layer, uint32_t level, uint32_t* w) {
+    Team* T = ctx->team_root;
+    const Plan& p0 = ctx->plan;
+    const uint32_t L = p0.log_n - layer, Lb = L - T->logG;
+    if (level > Lb) {
+        const uint32_t j = level - Lb;
+        const uint32_t* top = ctx->db.top + (size_t)layer * 2 * 64 * 8;
+        FRI_HIP(ctx, hipMemcpyAsync(w, top + 8 * level_offset(T->logG, j), ((size_t)1 << (T->logG - j)) * 32,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        return FRI_OK;
+    }
+    const size_t cnt = (size_t)1 << (Lb - level);     // digests of this level per block
+    for (uint32_t r = 0; r < T->G; r++) {
+        fri_ctx* c = T->rk[r];
+        const Plan& p = c->plan;
+        FRI_HIP(ctx, hipSetDevice(c->device));
+        FRI_HIP(ctx, hipMemcpyAsync(w + 8 * cnt * p.block[layer], p.trees + p.tree_off[layer] + 8 * level_offset(Lb, level),
+                                    cnt * 32, hipMemcpyDeviceToHost, c->stream));
+    }
+    for (uint32_t r = 0; r < T->G; r++) FRI_HIP(ctx, hipStreamSynchronize(T->rk[r]->stream));
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    return FRI_OK;
+}
+
+// fri_decommit_query on a team commit: every rank runs the sharded
+// decommitment (its openings, the peer all-gather, the max-combine); rank 0's
+// output is the caller's.
+static int team_decommit(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t values_cap, uint8_t* paths,
+                         size_t paths_cap, size_t* paths_len) {
+    Team* T = ctx->team_root;
+    std::vector<std::vector<uint32_t>> vals(T->G);
+    std::vector<std::vector<uint8_t>> pth(T->G);
+    std::vector<size_t> plen(T->G, 0);
+    for (uint32_t r = 1; r < T->G; r++) {
+        vals[r].assign(values_cap ? values_cap : 1, 0u);
+        pth[r].assign(paths_cap ? paths_cap : 1, 0u);
+    }
+    return team_run(ctx, [&](uint32_t r) {
+        if (r == 0) return decommit_sharded(ctx, index, values, values_cap, paths, paths_cap, paths_len);
+        return decommit_sharded(T->rk[r], index, vals[r].data(), values_cap, paths ? pth[r].data() : nullptr, paths_cap,
+                                &plen[r]);
+    });
 }

@@ -132,4 +132,29 @@ void launch_replicate(const uint32_t* src, uint32_t* dst, size_t words, uint32_t
     hipLaunchKernelGGL(k_replicate, dim3(blocks ? blocks : 1), dim3(256), 0, s, src, dst, words, G);
 }
 
+// In-process peer transport (fri_ctx_create_multi): rank r copies source p's
+// bytes (another rank's send buffer, on this device or, with peer access
+// enabled, read over xGMI from another one) to dst + p * words, for every
+// source p in one launch (grid.y = source).  16-byte accesses when every
+// pointer and the size allow them.
+__global__ __launch_bounds__(256) void k_peer_pull(PeerPull pp) {
+    const uint32_t p = blockIdx.y;
+    const uint32_t* __restrict__ src = pp.src[p];
+    uint32_t* __restrict__ dst = pp.dst + (size_t)p * pp.words;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pp.vec4) {
+        const size_t nv = pp.words >> 2;
+        for (; i < nv; i += stride) reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else {
+        for (; i < pp.words; i += stride) dst[i] = src[i];
+    }
+}
+void launch_peer_pull(const PeerPull& pp, hipStream_t s) {
+    const size_t units = pp.vec4 ? pp.words >> 2 : pp.words;
+    const size_t want = std::max<size_t>(1, (units + 1023) / 1024);          // ~4 units per thread
+    const uint32_t gx = (uint32_t)std::min<size_t>(want, std::max<size_t>(1, 2048 / std::max(1u, pp.n)));
+    hipLaunchKernelGGL(k_peer_pull, dim3(gx, pp.n), dim3(256), 0, s, pp);
+}
+
 }  // namespace fri

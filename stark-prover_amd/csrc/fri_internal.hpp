@@ -178,6 +178,17 @@ void launch_pair_fold(const uint32_t* first, const uint32_t* second, const uint3
 // layer[block_of[r] * B ..] = gath[r * B ..] for r < G (B a multiple of 4).
 void launch_place_blocks(const uint32_t* gath, uint32_t* layer, size_t B, uint32_t G, const uint32_t* block_of,
                          hipStream_t s);
+// In-process peer transport: dst[p * words ..] = src[p][0 .. words) for p < n
+// (n <= 64 sources, each another rank's buffer); vec4: every pointer 16-byte
+// aligned and words % 4 == 0.
+struct PeerPull {
+    const uint32_t* src[64];
+    uint32_t* dst;
+    size_t words;
+    uint32_t n;
+    uint32_t vec4;
+};
+void launch_peer_pull(const PeerPull& pp, hipStream_t s);
 // Loopback rehearsal: dst = G copies of src (words each), one launch.
 void launch_replicate(const uint32_t* src, uint32_t* dst, size_t words, uint32_t G, hipStream_t s);
 // Tree top + degree + channel step for a layer whose level `l` (2^(L-l)

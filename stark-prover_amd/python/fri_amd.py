@@ -77,6 +77,7 @@ class TransportOp(ctypes.Structure):
 
 
 TRANSPORT_OPS = {1: "allgather", 2: "alltoall", 3: "sendrecv"}
+TRANSPORTS = ("none", "rccl", "host", "loopback", "peer")     # FRI_TRANSPORT_* (fri_amd.h)
 
 _lib = None
 
@@ -94,6 +95,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     vp = ctypes.c_void_p
     sig = {
         "fri_ctx_create": (i32, [i32, u32, ctypes.POINTER(vp)]),
+        "fri_ctx_create_multi": (i32, [ctypes.POINTER(i32), u32, u32, i32, ctypes.POINTER(vp)]),
+        "fri_debug_team_rank": (i32, [vp, u32, ctypes.POINTER(vp)]),
         "fri_ctx_destroy": (i32, [vp]),
         "fri_last_error": (ctypes.c_char_p, [vp]),
         "fri_version": (ctypes.c_char_p, []),
@@ -147,6 +150,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                              ctypes.POINTER(sz)]),
         "fri_debug_loopback_degrees": (i32, [vp, ctypes.POINTER(ctypes.c_int32), u32]),
         "fri_ctx_set_lanes": (i32, [vp, u32]),
+        "fri_debug_ticket_lane": (i32, [vp, ctypes.c_uint64, ctypes.POINTER(i32)]),
         "fri_commit_degrees": (i32, [vp, ctypes.POINTER(ctypes.c_int32), sz, ctypes.POINTER(u32)]),
         "fri_debug_transport_log": (i32, [vp, ctypes.POINTER(TransportOp), sz, ctypes.POINTER(sz)]),
     }
@@ -175,22 +179,56 @@ def _ptr(a: np.ndarray):
 
 
 class Context:
-    """Owns one fri_ctx (device buffers, stream, graphs) on one GPU."""
+    """Owns one fri_ctx (device buffers, stream, graphs) on one GPU, or, from
+    ``Context.multi``, a team of ranks on several GPUs behind one context."""
 
-    def __init__(self, device: int = 0, log_n_max: int = 20):
+    def __init__(self, device: int = 0, log_n_max: int = 20, _handle=None, _owner=True):
         self.lib = load_library()
+        self.device = device
+        self.log_n_max = log_n_max
+        self.n_ranks = 1
+        self._owner = _owner
+        if _handle is not None:
+            self.h = _handle
+            return
         h = ctypes.c_void_p()
         rc = self.lib.fri_ctx_create(device, log_n_max, ctypes.byref(h))
         if rc != FRI_OK:
             raise FriError(rc, "fri_ctx_create failed (no gfx950 device?)")
         self.h = h
-        self.device = device
-        self.log_n_max = log_n_max
+
+    @classmethod
+    def multi(cls, devices: Sequence[int], log_n_max: int, transport: str = "auto") -> "Context":
+        """fri_ctx_create_multi: ONE context over len(devices) GPUs (ranks;
+        a device may repeat), driven from this thread.  commit / commit_device
+        of a codeword >= 2^20 run coset-sharded over the ranks in one call;
+        every read-back serves the whole commit.  transport: "auto" (RCCL if
+        it initialises, else peer), "rccl" or "peer"."""
+        lib = load_library()
+        kinds = {"auto": 0, "rccl": 1, "peer": 4}
+        if transport not in kinds:
+            raise FriError(FRI_EINVAL, f"transport must be one of {sorted(kinds)}")
+        devs = (ctypes.c_int * len(devices))(*[int(x) for x in devices])
+        h = ctypes.c_void_p()
+        rc = lib.fri_ctx_create_multi(devs, len(devices), log_n_max, kinds[transport], ctypes.byref(h))
+        if rc != FRI_OK:
+            raise FriError(rc, f"fri_ctx_create_multi({list(devices)}, {log_n_max}, {transport}) failed")
+        c = cls(int(devices[0]), log_n_max, _handle=h)
+        c.n_ranks = len(devices)
+        c.devices = [int(x) for x in devices]
+        return c
+
+    def team_rank(self, rank: int) -> "Context":
+        """A non-owning view of rank ``rank``'s context (fri_debug_team_rank),
+        for its transport log and device bytes."""
+        h = ctypes.c_void_p()
+        self._check(self.lib.fri_debug_team_rank(self.h, rank, ctypes.byref(h)))
+        return Context(self.device, self.log_n_max, _handle=h, _owner=False)
 
     def close(self):
-        if self.h:
+        if self.h and self._owner:
             self.lib.fri_ctx_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -304,10 +342,16 @@ class Context:
         return t.value
 
     def set_lanes(self, max_lanes: int):
-        """Commit lanes of the pipelined commits (fri_ctx_set_lanes): pending
-        commit i runs on lane (slot mod max_lanes), each lane a stream with its
-        own plan, so consecutive commits overlap on the device."""
+        """Commit lanes of the pipelined commits (fri_ctx_set_lanes): each
+        pending commit runs on the lane with the fewest pending commits, each
+        lane a stream with its own plan, so consecutive commits overlap."""
         self._check(self.lib.fri_ctx_set_lanes(self.h, max_lanes))
+
+    def ticket_lane(self, ticket: int) -> int:
+        """Lane a pending pipelined commit was dealt to (fri_debug_ticket_lane)."""
+        lane = ctypes.c_int()
+        self._check(self.lib.fri_debug_ticket_lane(self.h, ticket, ctypes.byref(lane)))
+        return lane.value
 
     def commit_wait(self, ticket: int, out: Optional[CommitResult] = None) -> CommitResult:
         """Wait for an enqueued commit and return its result (fri_commit_wait)."""
@@ -520,10 +564,10 @@ class Context:
 
     def dist_info(self):
         """(rank, world, transport) as the attached transport reports them
-        (transport: "none", "rccl", "host" or "loopback"; fri_dist_info)."""
+        (transport: "none", "rccl", "host", "loopback" or "peer"; fri_dist_info)."""
         r, w, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         self._check(self.lib.fri_dist_info(self.h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(t)))
-        return r.value, w.value, ("none", "rccl", "host", "loopback")[t.value]
+        return r.value, w.value, TRANSPORTS[t.value]
 
     def dist_selftest(self, words_per_peer: int = 4096):
         self._check(self.lib.fri_dist_selftest(self.h, words_per_peer))

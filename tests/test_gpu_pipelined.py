@@ -302,8 +302,8 @@ def test_python_mirror_pipelined_over_contexts(oracle, oracle_commit):
 
 
 def test_commit_lanes(pctx, oracle, oracle_commit, torch):
-    """Commit lanes (fri_ctx_set_lanes): pending commit i runs on lane
-    (slot mod max_lanes), a stream with its own plan.  With 1..4 lanes every
+    """Commit lanes (fri_ctx_set_lanes): a pending commit runs on the lane
+    with the fewest pending commits, a stream with its own plan.  With 1..4 lanes every
     transcript equals the oracle's; each lane in use holds one plan of HBM;
     the limits of include/fri_amd.h hold."""
     import fri_amd
@@ -352,8 +352,8 @@ def test_lanes_sync_commit_and_input_buffer(pctx, oracle, oracle_commit, torch):
     pctx.commit(c3, LOG_N)
     p0 = ctypes.c_void_p()
     pctx._check(pctx.lib.fri_ctx_input_buffer(pctx.h, d, ctypes.byref(p0)))
-    t1 = pctx.commit_device_async(b1.data_ptr(), d, LOG_N)          # slot 0: lane 0
-    t2 = pctx.commit_device_async(b2.data_ptr(), d, LOG_N)          # slot 1: lane 1
+    t1 = pctx.commit_device_async(b1.data_ptr(), d, LOG_N)          # lane 0
+    t2 = pctx.commit_device_async(b2.data_ptr(), d, LOG_N)          # lane 1
     assert _transcript(pctx.commit_wait(t1)) == oracle_commit(LOG_N, s1)
     sync = pctx.commit(c3, LOG_N)                                    # lane 0, beside lane 1's pending commit
     assert _transcript(sync) == oracle_commit(LOG_N, 1013)
@@ -402,6 +402,7 @@ def test_input_buffer_read_in_call_order_across_lanes(oracle, oracle_commit, tor
         tB = cx.commit_device_async(dQ.data_ptr(), d, L)                # slot 1: lane 1, a whole commit
         tC = cx.commit_device_async(dbad.data_ptr(), d, L)              # slot 2: lane 0, stages bad, stops early
         tD = cx.commit_device_async(p0.value, d, L)                     # slot 3: lane 1, reads the buffer
+        assert [cx.ticket_lane(t) for t in (tA, tB, tC, tD)] == [0, 1, 0, 1]
         for t in (tA, tC):
             with pytest.raises(fri_amd.FriError) as e:
                 cx.commit_wait(t)
@@ -413,9 +414,10 @@ def test_input_buffer_read_in_call_order_across_lanes(oracle, oracle_commit, tor
         resB = _transcript(cx.commit_wait(tB))
         # a valid staging just before D
         tA = cx.commit_device_async(dP3.data_ptr(), d, L)               # slot 0: lane 0, stages P3
-        tB2 = cx.commit_device_async(dQ.data_ptr(), d, L)               # slot 1: lane 1
+        tB2 = cx.commit_device_async(dQ.data_ptr(), d, L)               # lane 1
         tD = cx.commit_device_async(p0.value, d, L)                     # slot 2: lane 0 (reads it directly)
         tE = cx.commit_device_async(p0.value, d, L)                     # slot 3: lane 1, copy on lane 0's stream
+        assert [cx.ticket_lane(t) for t in (tA, tB2, tD, tE)] == [0, 1, 0, 1]
         cx.commit(cP2, L)                                               # stages P2 after all of them
         res = [_transcript(cx.commit_wait(t)) for t in (tA, tB2, tD, tE)]
     finally:
@@ -423,3 +425,62 @@ def test_input_buffer_read_in_call_order_across_lanes(oracle, oracle_commit, tor
     assert resB == oracle_commit(L, 2002)
     assert _transcript(sync) == oracle_commit(L, 2003)
     assert res == [oracle_commit(L, 2004), oracle_commit(L, 2002), oracle_commit(L, 2004), oracle_commit(L, 2004)]
+
+
+def test_lanes_balanced_at_depth_four(pctx, oracle, oracle_commit, torch):
+    """Four commits pending on three lanes: each new commit goes to the lane
+    with the fewest pending commits (ties: the lane dealt a commit longest
+    ago), so no lane holds two while another holds none, and the lanes rotate
+    instead of lane 0 taking two of every four (the slot-mod-lanes deal).
+    Every transcript equals the oracle's."""
+    d = (1 << LOG_N) >> 3
+    polys = _polys(oracle, torch, [1101, 1102, 1103])
+    want = {s: oracle_commit(LOG_N, s) for s, _ in polys}
+    pctx.set_lanes(3)
+    pend, lanes = [], []
+    for i in range(16):
+        s, buf = polys[i % 3]
+        t = pctx.commit_device_async(buf.data_ptr(), d, LOG_N)
+        pend.append((s, t))
+        load = [0, 0, 0]
+        for _, tt in pend:
+            load[pctx.ticket_lane(tt)] += 1
+        assert max(load) - min(load) <= 1, (i, load)
+        lanes.append(pctx.ticket_lane(t))
+        if len(pend) == 4:
+            s0, t0 = pend.pop(0)
+            assert _transcript(pctx.commit_wait(t0)) == want[s0]
+    for s0, t0 in pend:
+        assert _transcript(pctx.commit_wait(t0)) == want[s0]
+    # after the first four, every window of three consecutive commits uses all three lanes
+    for i in range(4, len(lanes) - 2):
+        assert sorted(lanes[i:i + 3]) == [0, 1, 2], lanes
+
+
+def test_rejected_sync_commit_keeps_pending_lane_commit_resident(pctx, oracle, oracle_commit, torch):
+    """A pipelined commit pending on lane 1, then a synchronous fri_commit
+    rejected for its arguments: the read-backs still serve the lane-1 commit
+    (its generation, its layers), not lane 0's older plan."""
+    import fri_amd
+    d = (1 << LOG_N) >> 3
+    (s0, b0), (s1, b1) = _polys(oracle, torch, [1111, 1112])
+    pctx.set_lanes(2)
+    pctx.commit(oracle.splitmix64_np(s0, d).astype(np.uint32), LOG_N)    # lane 0 resident: s0
+    t0 = pctx.commit_device_async(b0.data_ptr(), d, LOG_N)              # lane 0 (both idle: lower index)
+    t1 = pctx.commit_device_async(b1.data_ptr(), d, LOG_N)              # lane 1 (fewest pending)
+    assert {pctx.ticket_lane(t0), pctx.ticket_lane(t1)} == {0, 1}
+    gen = pctx.commit_info()[0]
+    for bad in (dict(log_n=LOG_N + 1), dict(offset=0)):
+        with pytest.raises(fri_amd.FriError) as e:
+            pctx.commit(oracle.splitmix64_np(s0, d).astype(np.uint32), bad.get("log_n", LOG_N),
+                        offset=bad.get("offset", fri_amd.GENERATOR))
+        assert e.value.code == fri_amd.FRI_EINVAL
+        g, ln, nl = pctx.commit_info()
+        assert (g, ln, nl) == (gen, LOG_N, LOG_N - 2)
+        root0 = bytes(pctx.tree_level(0, LOG_N, LOG_N)[0]).hex()
+        assert root0 == oracle_commit(LOG_N, s1)["roots"][0]            # the last enqueued commit
+        lay = pctx.layer(1, LOG_N)
+        val, _ = pctx.auth_path(1, 7, LOG_N)
+        assert int(val) == int(lay[7])
+    assert _transcript(pctx.commit_wait(t0)) == oracle_commit(LOG_N, s0)
+    assert _transcript(pctx.commit_wait(t1)) == oracle_commit(LOG_N, s1)

@@ -1,0 +1,235 @@
+"""Single-process multi-GPU context (fri_ctx_create_multi, include/fri_amd.h):
+ONE call of fri_commit (src/fri/fri_commit.rs:72-76) commits a codeword
+coset-sharded over a team of ranks driven from this one host thread.
+
+On the 1-GPU box every rank sits on GPU 0 and the team uses the peer
+transport (device copies between the ranks' buffers, ordered by events), the
+same kernels and schedule as on G devices; only the xGMI reads become local
+ones.  Every transcript is compared with the C oracle's (bit-exact), every
+read-back of a sharded layer with a 1-GPU commit of the same polynomial, and
+every rank's transport log with the deadlock-freedom condition of DESIGN.md §7."""
+import ctypes
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def _transcript(res):
+    return {"roots": [bytes(res.roots[k]).hex() for k in range(res.n_layers)],
+            "betas": [int(res.betas[r]) for r in range(res.n_rounds)],
+            "final_value": int(res.final_value), "final_degree": int(res.final_degree),
+            "state": bytes(res.channel_out.digest).hex()}
+
+
+def _coeffs(oracle, seed, log_n, blowup_log=3):
+    return oracle.splitmix64_np(seed, (1 << log_n) >> blowup_log).astype(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def team4():
+    import fri_amd
+    c = fri_amd.Context.multi([0, 0, 0, 0], 23, transport="peer")
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def one24():
+    import fri_amd
+    c = fri_amd.Context(0, 24)
+    yield c
+    c.close()
+
+
+def test_team_info_and_selftest(team4):
+    assert team4.dist_info() == (0, 4, "peer")
+    for r in range(4):
+        assert team4.team_rank(r).dist_info() == (r, 4, "peer")
+    team4.dist_selftest(4096)
+    for r in range(4):
+        ops = [op for _, op, _, _ in team4.team_rank(r).transport_log()]
+        assert ops == ["alltoall", "allgather", "sendrecv"]
+
+
+@pytest.mark.parametrize("log_n,seed", [(20, 5), (22, 42), (23, 7)])
+def test_team4_commit_matches_oracle(team4, oracle, oracle_commit, log_n, seed):
+    """fri_commit on the team context: the whole transcript equals the C
+    oracle's (one call; ranks 1-3 on the context's worker threads)."""
+    from test_dist import check_transport_schedule
+    res = team4.commit(_coeffs(oracle, seed, log_n), log_n)
+    assert _transcript(res) == oracle_commit(log_n, seed)
+    logs = [team4.team_rank(r).transport_log() for r in range(4)]
+    check_transport_schedule(logs)
+    assert sum(1 for e in logs[0] if e[1] == "alltoall") == 1
+
+
+@pytest.mark.parametrize("G,log_n", [(2, 21), (8, 24)])
+def test_team_sizes_match_oracle(oracle, oracle_commit, G, log_n):
+    """G = 2 (radix-2 layer 0, no all-to-all) and G = 8 (a shard-sized 2^21
+    rank context), on one GPU over the peer transport."""
+    import fri_amd
+    cx = fri_amd.Context.multi([0] * G, log_n, transport="peer")
+    try:
+        for seed in (42, 43):
+            assert _transcript(cx.commit(_coeffs(oracle, seed, log_n), log_n)) == oracle_commit(log_n, seed)
+        # each rank holds about 1/G of the plan: rank 1's HBM well below the
+        # 1-GPU plan's layers + trees + x^-1 tables (host-side layout)
+        r1 = cx.team_rank(1).device_bytes()[1]
+        full = fri_amd.plan_layout((1 << log_n) >> 3, log_n)["bytes"]
+        assert r1 < full * (0.5 if G == 8 else 0.8), (r1, full)
+    finally:
+        cx.close()
+
+
+def test_team_readbacks_equal_single_gpu(team4, one24, oracle):
+    """Every read-back of the team commit (layers, tree levels below and
+    above the block roots, authentication paths, whole decommitments) equals
+    the 1-GPU commit's of the same polynomial."""
+    L = 22
+    cf = _coeffs(oracle, 99, L)
+    r1 = one24.commit(cf, L)
+    rt = team4.commit(cf, L)
+    assert _transcript(rt) == _transcript(r1)
+    n_layers = rt.n_layers
+    for k in (0, 1, 2, 3, n_layers - 1):
+        assert np.array_equal(team4.layer(k, L), one24.layer(k, L)), k
+    for k in (0, 2):
+        Lk = L - k
+        for lvl in (0, 1, Lk - 3, Lk - 2, Lk - 1, Lk):
+            assert team4.tree_level(k, lvl, L) == one24.tree_level(k, lvl, L), (k, lvl)
+    for k, idx in ((0, 12345), (1, (1 << 21) - 1), (2, 777)):
+        assert team4.auth_path(k, idx, L) == one24.auth_path(k, idx, L)
+    for idx in (0, 31337, (1 << 22) - 5):
+        assert team4.decommit_query(idx, n_layers, L) == one24.decommit_query(idx, n_layers, L)
+    g, ln, nl = team4.commit_info()
+    assert (ln, nl) == (L, n_layers)
+    assert team4.commit_degrees() == one24.commit_degrees()
+
+
+def test_team_python_mirror_unchanged(team4, one24, oracle, oracle_commit):
+    """The reference-shaped surface (fri_amd.fri_commit / decommit_fri /
+    verify_fri, the Python twin of the Rust shim in INTEGRATION.md) takes the
+    team context unchanged: the commit's messages equal the C oracle's, and
+    the whole transcript with two decommitments equals a 1-GPU context's."""
+    import fri_amd
+    L = 21
+    coeffs = _coeffs(oracle, 3, L)
+    chans = []
+    for cx in (team4, one24):
+        ch = fri_amd.Channel()
+        proof = fri_amd.fri_commit(coeffs, L, ch, ctx=cx)
+        assert ch.state == oracle_commit(L, 3)["state"]
+        fri_amd.decommit_fri(2, (1 << L) - 1, proof, ch)
+        assert fri_amd.verify_fri(ch.proof, L, proof.n_layers, 2, (1 << L) - 1)
+        chans.append(ch)
+    assert chans[0].proof == chans[1].proof and chans[0].state == chans[1].state
+
+
+def test_team_small_codeword_runs_on_rank0(team4, oracle, oracle_commit):
+    """A codeword below the sharding threshold (2^20) runs on rank 0 alone:
+    the other ranks issue no collective, and the layers read back whole."""
+    team4.commit(_coeffs(oracle, 8, 21), 21)
+    before = team4.team_rank(1).transport_log()
+    res = team4.commit(_coeffs(oracle, 11, 16), 16)
+    assert _transcript(res) == oracle_commit(16, 11)
+    assert team4.team_rank(1).transport_log() == before
+    assert np.array_equal(team4.layer(0, 16), team4.lde(_coeffs(oracle, 11, 16), 16))
+
+
+def test_team_errors_then_recovers(team4, oracle, oracle_commit):
+    """A non-canonical coefficient fails the team commit with FRI_EINVAL on
+    every rank (checked on the device), forced betas reach every rank, and the
+    team commits correctly afterwards; the pipelined and attach calls are
+    refused on a team context."""
+    import fri_amd
+    L = 21
+    bad = _coeffs(oracle, 5, L)
+    bad[1000] = fri_amd.P
+    with pytest.raises(fri_amd.FriError) as e:
+        team4.commit(bad, L)
+    assert e.value.code == fri_amd.FRI_EINVAL
+    assert team4.commit_info()[2] == 0
+    betas = [(i * 7919 + 11) % fri_amd.P for i in range(fri_amd.MAX_ROUNDS)]
+    r = team4.commit(_coeffs(oracle, 5, L), L, forced_betas=betas)
+    one = fri_amd.Context(0, L)
+    try:
+        assert _transcript(r) == _transcript(one.commit(_coeffs(oracle, 5, L), L, forced_betas=betas))
+    finally:
+        one.close()
+    assert _transcript(team4.commit(_coeffs(oracle, 5, L), L)) == oracle_commit(L, 5)
+    with pytest.raises(fri_amd.FriError) as e:
+        team4.commit_async(_coeffs(oracle, 5, L), L)
+    assert e.value.code == fri_amd.FRI_EINVAL
+    with pytest.raises(fri_amd.FriError) as e:
+        team4.attach_loopback(0, 2)
+    assert e.value.code == fri_amd.FRI_EINVAL
+    with pytest.raises(fri_amd.FriError) as e:
+        team4.detach()
+    assert e.value.code == fri_amd.FRI_EINVAL
+
+
+def test_team_commit_device_from_rank0_buffer(team4, oracle, oracle_commit):
+    """fri_commit_device on the team: the context's input buffer (rank 0's
+    device) is read by rank 0 in place and copied by the other ranks."""
+    import fri_amd
+    L = 22
+    cf = _coeffs(oracle, 42, L)
+    team4.commit(cf, L)
+    p = ctypes.c_void_p()
+    team4._check(team4.lib.fri_ctx_input_buffer(team4.h, cf.size, ctypes.byref(p)))
+    out = fri_amd.CommitResult()
+    for _ in range(3):
+        team4._check(team4.lib.fri_commit_device(team4.h, p, cf.size, L, fri_amd.GENERATOR, None, 0, None,
+                                                 ctypes.byref(out)))
+        assert _transcript(out) == oracle_commit(L, 42)
+
+
+def test_team_create_arguments():
+    import fri_amd
+    with pytest.raises(fri_amd.FriError):
+        fri_amd.Context.multi([0, 0, 0], 22)                  # not a power of two
+    with pytest.raises(fri_amd.FriError):
+        fri_amd.Context.multi([0, 0], 22, transport="rccl")   # ranks share a device: RCCL cannot run them
+    with pytest.raises(fri_amd.FriError):
+        fri_amd.Context.multi([0, 99], 22)                    # no such device
+    c = fri_amd.Context.multi([0], 16)                        # one device: an ordinary context
+    try:
+        assert c.dist_info()[2] == "none"
+    finally:
+        c.close()
+
+
+@pytest.mark.timeout(1200)
+def test_team_2p28_world8_configs4(oracle_commit):
+    """BASELINE configs[4]: the 2^28 codeword committed coset-sharded over 8
+    ranks by ONE fri_commit call on a team context (peer transport, every
+    rank on GPU 0: 8 shard-sized plans, ~50 GB), bit-exact against the C
+    oracle; every decommitment layer checks against its root."""
+    import fri_amd
+    import fri_oracle as fo
+    L = 28
+    cf = fo.splitmix64_np(42, (1 << L) >> 3).astype(np.uint32)
+    cx = fri_amd.Context.multi([0] * 8, L, transport="peer")
+    try:
+        res = cx.commit(cf, L)
+        want = oracle_commit(L, 42)
+        assert _transcript(res) == want
+        q = cx.decommit_query(123456789, res.n_layers, L)
+        for k, (v, sv, path, spath) in enumerate(q):
+            m = 1 << (L - k)
+            i = 123456789 % m
+            h = hashlib.sha256(int(v).to_bytes(8, "big")).digest()
+            for lvl in range(L - k):
+                sib = path[32 * lvl:32 * lvl + 32]
+                h = hashlib.sha256(sib + h if (i >> lvl) & 1 else h + sib).digest()
+            assert h.hex() == want["roots"][k], k
+    finally:
+        cx.close()
