@@ -107,7 +107,8 @@ struct DistBuf {
     size_t cap = 0;             // words in cyc/recv
     uint32_t* cyc = nullptr;    // coset slice / all-to-all send
     uint32_t* recv = nullptr;   // all-to-all / gather receive
-    uint32_t* half = nullptr;   // partner half-block
+    uint32_t* half = nullptr;   // partner half-block (even layers' exchanges)
+    uint32_t* half2 = nullptr;  // partner half-block (odd layers': the fused leaf kernel still reads the other)
     uint32_t* top = nullptr;    // per-layer top trees (2G digests each)
     uint32_t* pre_lo = nullptr; // coset pre-scale tables
     uint32_t* pre_hi = nullptr;
@@ -465,7 +466,7 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     }
     for (auto e : ctx->event_pool) hipEventDestroy(e);
     fri_dist_detach(ctx);
-    dfree(ctx, ctx->db.cyc); dfree(ctx, ctx->db.recv); dfree(ctx, ctx->db.half);
+    dfree(ctx, ctx->db.cyc); dfree(ctx, ctx->db.recv); dfree(ctx, ctx->db.half); dfree(ctx, ctx->db.half2);
     dfree(ctx, ctx->db.top); dfree(ctx, ctx->db.pre_lo); dfree(ctx, ctx->db.pre_hi); dfree(ctx, ctx->db.gath);
     dfree(ctx, ctx->db.dq); dfree(ctx, ctx->db.rec); dfree(ctx, ctx->db.shtop);
     if (ctx->xstream) hipStreamDestroy(ctx->xstream);
@@ -2298,12 +2299,13 @@ static int dist_buffers(fri_ctx* ctx, size_t M, uint32_t G, size_t gwords) {
     DistBuf& b = ctx->db;
     const size_t nhi = 1u << 20;   // pow table hi part, generous (M <= 2^32)
     if (b.cap < M) {
-        dfree(ctx, b.cyc); dfree(ctx, b.recv); dfree(ctx, b.half);
-        b.cyc = b.recv = b.half = nullptr;
+        dfree(ctx, b.cyc); dfree(ctx, b.recv); dfree(ctx, b.half); dfree(ctx, b.half2);
+        b.cyc = b.recv = b.half = b.half2 = nullptr;
         b.cap = 0;
         FRI_HIP(ctx, dalloc(ctx, &b.cyc, M * 4));
         FRI_HIP(ctx, dalloc(ctx, &b.recv, M * 4));
         FRI_HIP(ctx, dalloc(ctx, &b.half, (M / 2 + 1) * 4));
+        FRI_HIP(ctx, dalloc(ctx, &b.half2, (M / 4 + 1) * 4));   // odd layers: half of a block of layer >= 1
         b.cap = M;
     }
     // (each lazily created member on its own, as in async_enqueue)
@@ -2450,6 +2452,14 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
     }
     std::vector<uint32_t> block_of(G), rank_of(G);
     for (uint32_t r = 0; r < G; r++) block_of[r] = rank_of[r] = r;
+    // The fold of sharded layer k-1 into this rank's block of layer k runs
+    // inside layer k's leaf kernel (fold, leaves, levels 1-4 in one pass, as
+    // on one GPU): its operands, the local and the partner's half-blocks.
+    // (It was a separate k_pair_fold launch with a write and a re-read of
+    // every folded block.)
+    const uint32_t* f_first = nullptr;
+    const uint32_t* f_second = nullptr;
+    const uint32_t* f_xi = nullptr;
     int k = 0;
     for (;; k++) {
         const uint32_t Lk = log_n - (uint32_t)k;        // full layer size 2^Lk
@@ -2457,22 +2467,34 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         uint32_t* vals = p.layers + p.layer_off[k];     // my block at the start of the layer slot
         const bool last = (k == p.rmax);
         const bool next_sharded = next_layer_sharded(log_n, logG, k, p.rmax);
-        // exchange of the half-block the partner needs for the next fold (overlaps the local tree)
+        const bool fused = f_first != nullptr;          // this layer's block is folded by its leaf kernel
+        // exchange of the half-block the partner needs for the next fold
+        // (overlaps the rest of the layer's tree); its receive buffer
+        // alternates with the layer, because layer k+1's leaf kernel still
+        // reads the partner half of exchange k while exchange k+1 lands
         const uint32_t b = block_of[rank];
         const bool isA = b < G / 2;
         const uint32_t partner = isA ? rank_of[b + G / 2] : rank_of[b - G / 2];
-        if (next_sharded) {
+        uint32_t* half_in = (k & 1) ? db.half2 : db.half;
+        auto exchange = [&]() -> int {
             if (!ctx->tp.host) {
                 FRI_HIP(ctx, hipEventRecord(ctx->ev_vals, s));
                 FRI_HIP(ctx, hipStreamWaitEvent(ctx->xstream, ctx->ev_vals, 0));
-                rc = tp_sendrecv(ctx, isA ? vals + B / 2 : vals, db.half, (B / 2) * 4, (int)partner, ctx->xstream, 1);
-                if (rc) return rc;
+                const int r2 = tp_sendrecv(ctx, isA ? vals + B / 2 : vals, half_in, (B / 2) * 4, (int)partner,
+                                           ctx->xstream, 1);
+                if (r2) return r2;
                 FRI_HIP(ctx, hipEventRecord(ctx->ev_xchg, ctx->xstream));
-            } else {
-                rc = tp_sendrecv(ctx, isA ? vals + B / 2 : vals, db.half, (B / 2) * 4, (int)partner, s, 1);
-                if (rc) return rc;
+                return FRI_OK;
             }
-        }
+            return tp_sendrecv(ctx, isA ? vals + B / 2 : vals, half_in, (B / 2) * 4, (int)partner, s, 1);
+        };
+        // layer 0's block is complete before its tree starts: exchange first;
+        // a fused layer's block is made by its leaf kernel: the exchange goes
+        // between the launch of the half it sends and the other half's
+        int xrc = FRI_OK;
+        if (next_sharded && !fused && (rc = exchange())) return rc;
+        std::function<void()> after_part1;
+        if (next_sharded && fused) after_part1 = [&]() { xrc = exchange(); };
         // block-local tree (levels 0 .. log2 B), gated on round k-1
         LayerTask tl{};
         tl.values = vals;
@@ -2480,6 +2502,14 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         tl.L = Lk - logG;
         tl.gst = ctx->d_state;
         tl.gidx = k > 0 ? k - 1 : -1;
+        if (fused) {
+            // the partner's half-block of layer k-1 (exchange k-1) has landed
+            if (!ctx->tp.host) FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_xchg, 0));
+            tl.prev = f_first;
+            tl.prev2 = f_second;
+            tl.xinv = f_xi;
+            tl.send_half = isA ? 1u : 0u;
+        }
         uint64_t leaf_nodes = 0;
         for (uint32_t j = 0; j <= 4 && j <= tl.L; j++) leaf_nodes += (uint64_t)1 << (tl.L - j);
         size_t spl = (k == 0 && tl.L >= 19) ? span_begin(ctx, "merkle_layer0_leaf", ((uint64_t)4 << tl.L) + 32 * leaf_nodes)
@@ -2524,7 +2554,8 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         tl.shard = db.shtop + k;
         launch_layer(tl, s, side ? ctx->ev_pre : (spl == (size_t)-1 ? nullptr : ctx->spans[spl].e),
                      side ? std::function<void()>(coef_beside) : std::function<void()>(),
-                     side ? ctx->ev_coef : nullptr);
+                     side ? ctx->ev_coef : nullptr, after_part1);
+        if (xrc) return xrc;
         FRI_HIP(ctx, beside_err);
         FRI_HIP(ctx, hipGetLastError());
         // all ranks' records; the replicated top reads the block roots (in
@@ -2539,14 +2570,15 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
         span_end(ctx, spk);
         if (last) break;
         if (next_sharded) {
-            if (!ctx->tp.host) FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_xchg, 0));
-            const uint32_t* first = isA ? vals : db.half;
-            const uint32_t* second = isA ? db.half : vals + B / 2;
+            // fold pairs (i, i + m/2): this rank's first operands are its own
+            // block's first half (A) or the partner's (B), the second ones the
+            // partner's second half (A) or its own (B); layer k+1's leaf kernel folds them
+            f_first = isA ? vals : half_in;
+            f_second = isA ? half_in : vals + B / 2;
             // the plan's slot k holds exactly this rank's x^-1 half-block slice
             if (fold_xinv_start(b, G, B) != p.xinv_start[k])
                 return fail(ctx, FRI_ESTATE, "shard plan out of step with the block schedule");
-            const uint32_t* xi = p.xinv + p.xinv_off[k];
-            launch_pair_fold(first, second, xi, p.layers + p.layer_off[k + 1], B / 2, ctx->d_state, k, s);
+            f_xi = p.xinv + p.xinv_off[k];
             advance_blocks(block_of, rank_of, G);
             continue;
         }
@@ -2587,6 +2619,12 @@ static int run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const u
             }
             return FRI_OK;
         };
+        // peer transport: every rank has issued its last collective's waits
+        // before any rank starts capturing the tail graph on its stream (HIP
+        // refuses a wait on an event of a stream that is capturing, even when
+        // the event was recorded before the capture began)
+        if (ctx->tp.peer && !team_barrier(ctx->tp.team))
+            return fail(ctx, FRI_ERCCL, "peer transport: another rank failed (" + ctx->tp.team->why + ")");
         if (ctx->profiling || (flags & FRI_FLAG_NO_GRAPH)) {
             if ((rc = local_tail())) return rc;
         } else {

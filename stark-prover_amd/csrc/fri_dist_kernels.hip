@@ -6,8 +6,9 @@
 //                        NTT with pre-scale s^j  ->  evals[r + G*m], m < M
 //   cyclic -> block     : after the all-to-all, rank g holds chunk t of every
 //                        rank's slice; block[G*t + r] = recv[r][t]
-//   pair fold           : layer k -> k+1 from the local half-block and the
-//                        partner's half-block (fri_commit.rs:53-65)
+//   (the pair fold of layer k -> k+1 from the local and the partner's
+//    half-blocks, fri_commit.rs:53-65, runs inside layer k+1's leaf kernel:
+//    k_layer_leaf<..., PAIR>, fri_layer.hip)
 //   (the per-layer records of block roots and coefficient maxima are written
 //    and read by the sharded top kernels, k_tree_top<..., SHARD>, fri_layer.hip)
 #include <algorithm>
@@ -16,7 +17,6 @@
 
 namespace fri {
 
-constexpr uint32_t INV2_MD = 0x80000000u;   // Montgomery(2^-1)
 
 // out[j] = sum_t a[j + t*M] * c^t for j < M  (c = s^M, Montgomery c_m).
 __global__ void k_coset_coeffs(const uint32_t* __restrict__ a, size_t d, uint32_t* __restrict__ out, size_t M,
@@ -51,23 +51,6 @@ __global__ void k_cyclic_to_block(const uint32_t* __restrict__ recv, uint32_t* _
 void launch_cyclic_to_block(const uint32_t* recv, uint32_t* block, size_t B, uint32_t G, hipStream_t s) {
     const size_t per = B / G;
     hipLaunchKernelGGL(k_cyclic_to_block, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, recv, block, per, G);
-}
-
-// out[j] = fold(first[j], second[j], xinv[j], beta_r), gated on active[r].
-__global__ void k_pair_fold(const uint32_t* __restrict__ first, const uint32_t* __restrict__ second,
-                            const uint32_t* __restrict__ xinv, uint32_t* __restrict__ out, size_t h,
-                            const DevState* __restrict__ st, int r) {
-    if (!st->active[r]) return;
-    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= h) return;
-    const uint32_t a = first[j], b = second[j];
-    const uint32_t s = add(a, b), t = sub(a, b);
-    out[j] = mmul(add(s, mmul(mmul(t, xinv[j]), st->beta_mont[r])), INV2_MD);
-}
-void launch_pair_fold(const uint32_t* first, const uint32_t* second, const uint32_t* xinv, uint32_t* out, size_t h,
-                      const DevState* st, int r, hipStream_t s) {
-    hipLaunchKernelGGL(k_pair_fold, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, s, first, second, xinv, out, h,
-                       st, r);
 }
 
 // G = 2, layer 0 without an all-to-all (radix-2 decimation): even/odd

@@ -154,13 +154,26 @@ struct LayerTask {
     // input at k == 0), coef_out[0] global coefficient obase of poly_k.
     size_t jlo, jhi, ibase, obase;
     const ShardTop* shard;     // sharded layer (device): nullptr otherwise
+    // Sharded block tree with the pair fold fused in (run_commit_sharded):
+    // the fold's second operand is prev2[i] (the partner's half-block)
+    // instead of prev[i + 2^L]; beta is gst->beta_mont[gidx].  The leaf
+    // kernel then runs as two launches, the half-block the next exchange
+    // sends (send_half: 0 first half, 1 second half) first.
+    const uint32_t* prev2;
+    uint32_t send_half;
+    uint32_t wg_base;          // (set per launch) first workgroup of a split launch
+    uint32_t wg_total;         // (set per launch) workgroups of the whole layer
 };
 // after_leaf: called right after the leaf kernel is enqueued (and
 // ev_leaf_end recorded), so the caller can start work on another stream
 // behind it; ev_before_top: the stream waits for it before the top kernel
 // (a sharded block top reads the coefficient maxima made on that stream).
+// after_part1 (a fused sharded layer, t.prev2 set): called right after the
+// leaf launch of the half-block the next exchange sends, so the caller can
+// enqueue that exchange while the other half is hashed.
 void launch_layer(const LayerTask& t, hipStream_t s, hipEvent_t ev_leaf_end = nullptr,
-                  const std::function<void()>& after_leaf = {}, hipEvent_t ev_before_top = nullptr);
+                  const std::function<void()>& after_leaf = {}, hipEvent_t ev_before_top = nullptr,
+                  const std::function<void()>& after_part1 = {});
 // Layers ts[0..n) (consecutive, 2^L <= 2^TAIL_LOG elements, commit mode) in
 // one single-workgroup launch (k_tree_tail), n <= TAIL_LOG + 1.
 void launch_tail(const LayerTask* ts, uint32_t n, hipStream_t s);
@@ -173,8 +186,6 @@ void launch_decimate(const uint32_t* a, size_t d, uint32_t* ev, uint32_t* od, hi
 void launch_radix2_block(const uint32_t* E, const uint32_t* O, const uint32_t* tlo, const uint32_t* thi,
                          uint32_t* out, size_t M, uint32_t negate, hipStream_t s);
 void launch_cyclic_to_block(const uint32_t* recv, uint32_t* block, size_t B, uint32_t G, hipStream_t s);
-void launch_pair_fold(const uint32_t* first, const uint32_t* second, const uint32_t* xinv, uint32_t* out, size_t h,
-                      const DevState* st, int r, hipStream_t s);
 // layer[block_of[r] * B ..] = gath[r * B ..] for r < G (B a multiple of 4).
 void launch_place_blocks(const uint32_t* gath, uint32_t* layer, size_t B, uint32_t G, const uint32_t* block_of,
                          hipStream_t s);

@@ -242,20 +242,25 @@ __device__ __forceinline__ bool gated_off(const LayerTask& t) {
     return t.gst && t.gidx >= 0 && !t.gst->active[t.gidx];
 }
 
+// PAIR: a sharded block tree with the pair fold fused in (LayerTask::prev2),
+// launched as a part of the layer's workgroups (wg_base).
+__device__ __forceinline__ uint32_t pair_beta(const LayerTask& t) { return t.gst->beta_mont[t.gidx]; }
+
 // TPB threads, 4 leaves each: 4*TPB leaves -> TPB/4 level-4 nodes per WG.
-template <bool FOLD, bool COMMIT, uint32_t TPB>
+template <bool FOLD, bool COMMIT, uint32_t TPB, bool PAIR = false>
 __global__ __launch_bounds__(TPB) void k_layer_leaf(LayerTask t) {
     if (gated_off(t)) return;
     __shared__ uint4 lds[3 * TPB];
     __shared__ int32_t red[3 * (TPB / 64)];
     const uint32_t L = t.L;
-    const size_t q = (size_t)blockIdx.x * TPB + threadIdx.x;   // quad index: leaves 4q..4q+3
+    const size_t wg = PAIR ? (size_t)blockIdx.x + t.wg_base : (size_t)blockIdx.x;
+    const size_t q = wg * TPB + threadIdx.x;   // quad index: leaves 4q..4q+3
     uint4 v;
     if (FOLD) {
         const size_t half = (size_t)1 << L;
-        const uint32_t beta_m = COMMIT ? t.st->beta_mont[t.k - 1] : t.beta_m;
+        const uint32_t beta_m = COMMIT ? t.st->beta_mont[t.k - 1] : (PAIR ? pair_beta(t) : t.beta_m);
         uint4 a = reinterpret_cast<const uint4*>(t.prev)[q];
-        uint4 b = reinterpret_cast<const uint4*>(t.prev + half)[q];
+        uint4 b = reinterpret_cast<const uint4*>(PAIR ? t.prev2 : t.prev + half)[q];
         uint4 x = reinterpret_cast<const uint4*>(t.xinv)[q];
         v.x = fold1(a.x, b.x, x.x, beta_m); v.y = fold1(a.y, b.y, x.y, beta_m);
         v.z = fold1(a.z, b.z, x.z, beta_m); v.w = fold1(a.w, b.w, x.w, beta_m);
@@ -268,7 +273,7 @@ __global__ __launch_bounds__(TPB) void k_layer_leaf(LayerTask t) {
     quad<true>(v, nullptr, tr + 8 * level_offset(L, 0), tr + 8 * level_offset(L, 1), q, top);
     if (COMMIT) coef_task(t, blockIdx.x, gridDim.x, red);
     lds_two_levels<TPB>(lds, top, tr + 8 * level_offset(L, 2), tr + 8 * level_offset(L, 3),
-                        tr + 8 * level_offset(L, 4), (size_t)blockIdx.x * TPB);
+                        tr + 8 * level_offset(L, 4), wg * TPB);
 }
 
 // Levels of the wide leaf kernel with fewer than WIDE_PAIR_MAX nodes in the
@@ -284,18 +289,20 @@ __host__ __device__ __forceinline__ uint32_t wide_levels(uint32_t L) { return L 
 // Wide leaf kernel for narrow layers (2^10 .. 2^18 elements): one leaf per
 // lane, 256 leaves per workgroup, levels 1..4 through LDS (one node per lane
 // per level): latency 1 leaf + 4 nodes instead of the quad form's 4 + 5.
-template <bool FOLD, bool COMMIT>
+template <bool FOLD, bool COMMIT, bool PAIR = false>
 __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
     if (gated_off(t)) return;
     __shared__ uint4 lds[2 * 256 + 2 * 128];
     __shared__ int32_t red[12];
     const uint32_t L = t.L;
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t wg = PAIR ? (size_t)blockIdx.x + t.wg_base : (size_t)blockIdx.x;
+    const size_t grid = PAIR ? (size_t)t.wg_total : (size_t)gridDim.x;   // the whole layer's workgroups
+    const size_t i = wg * 256 + threadIdx.x;
     uint32_t v;
     if (FOLD) {
         const size_t half = (size_t)1 << L;
-        const uint32_t beta_m = COMMIT ? t.st->beta_mont[t.k - 1] : t.beta_m;
-        v = fold1(t.prev[i], t.prev[i + half], t.xinv[i], beta_m);
+        const uint32_t beta_m = COMMIT ? t.st->beta_mont[t.k - 1] : (PAIR ? pair_beta(t) : t.beta_m);
+        v = fold1(t.prev[i], PAIR ? t.prev2[i] : t.prev[i + half], t.xinv[i], beta_m);
         t.values[i] = v;
     } else {
         v = t.values[i];
@@ -311,13 +318,13 @@ __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
     lds_barrier();
     uint32_t cnt = 256;
     const shaq::Role qr = shaq::role_of(threadIdx.x);
-    if ((size_t)gridDim.x * 128 < WIDE_PAIR_MAX) chain_prio();   // from level 1 on, all on lane pairs
+    if (grid * 128 < WIDE_PAIR_MAX) chain_prio();   // from level 1 on, all on lane pairs
     const uint32_t nlev = wide_levels(L);
 #pragma unroll 1
     for (uint32_t j = 1; j <= nlev; j++) {
         cnt >>= 1;
-        uint32_t* out = tr + 8 * (level_offset(L, j) + ((size_t)blockIdx.x << (8 - j)));
-        if ((size_t)cnt * gridDim.x < WIDE_PAIR_MAX) {
+        uint32_t* out = tr + 8 * (level_offset(L, j) + (wg << (8 - j)));
+        if ((size_t)cnt * grid < WIDE_PAIR_MAX) {
             pair_level(A, B, out, threadIdx.x, cnt, qr);   // latency-bound level: node per lane pair
         } else if (threadIdx.x < cnt) {
             Dg a, b, o;
@@ -1017,12 +1024,33 @@ static LayerTask with_gate(const LayerTask& in) {
 #define QUAD_MIN_LOG 19      // smaller layers: one leaf per lane (A/B: 19 beats 20 and 21)
 #endif
 
+// A fused sharded block tree's leaf kernel (PAIR): the layer's G workgroups
+// as two launches of G/2, the half-block the next exchange sends first, with
+// after_part1 in between (a single launch without it).
+template <typename KernelLaunch>
+static void pair_parts(LayerTask t, uint32_t G, hipStream_t s, const std::function<void()>& after_part1,
+                       KernelLaunch&& go) {
+    t.wg_total = G;
+    if (!after_part1) {
+        t.wg_base = 0;
+        go(t, G);
+        return;
+    }
+    const uint32_t h = G / 2;
+    t.wg_base = t.send_half ? h : 0u;
+    go(t, h);
+    after_part1();
+    t.wg_base = t.send_half ? 0u : h;
+    go(t, h);
+}
+
 void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end, const std::function<void()>& after_leaf,
-                  hipEvent_t ev_before_top) {
+                  hipEvent_t ev_before_top, const std::function<void()>& after_part1) {
     const LayerTask t = with_gate(tin);
     const uint32_t L = t.L;
     const bool fold = t.prev != nullptr;
     const bool commit = t.st != nullptr;
+    const bool pair = t.prev2 != nullptr;          // sharded block tree, pair fold fused (never commit mode)
     const int32_t* nomx = nullptr;
     if (L <= TOP_LOG) {
         if (fold) {
@@ -1040,7 +1068,11 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end, c
         constexpr uint32_t TPB = QUAD_TPB;
         G = (uint32_t)(((size_t)1 << L) / (4 * TPB));
         out_per_wg = TPB / 4;
-        if (fold) {
+        if (pair) {
+            pair_parts(t, G, s, after_part1, [&](const LayerTask& tp, uint32_t g) {
+                hipLaunchKernelGGL((k_layer_leaf<true, false, TPB, true>), dim3(g), dim3(TPB), 0, s, tp);
+            });
+        } else if (fold) {
             if (commit) hipLaunchKernelGGL((k_layer_leaf<true, true, TPB>), dim3(G), dim3(TPB), 0, s, t);
             else hipLaunchKernelGGL((k_layer_leaf<true, false, TPB>), dim3(G), dim3(TPB), 0, s, t);
         } else {
@@ -1050,7 +1082,11 @@ void launch_layer(const LayerTask& tin, hipStream_t s, hipEvent_t ev_leaf_end, c
     } else {
         G = 1u << (L - 8);
         out_per_wg = 256u >> wide_levels(L);
-        if (fold) {
+        if (pair) {
+            pair_parts(t, G, s, after_part1, [&](const LayerTask& tp, uint32_t g) {
+                hipLaunchKernelGGL((k_layer_leaf_wide<true, false, true>), dim3(g), dim3(256), 0, s, tp);
+            });
+        } else if (fold) {
             if (commit) hipLaunchKernelGGL((k_layer_leaf_wide<true, true>), dim3(G), dim3(256), 0, s, t);
             else hipLaunchKernelGGL((k_layer_leaf_wide<true, false>), dim3(G), dim3(256), 0, s, t);
         } else {
