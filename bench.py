@@ -561,9 +561,10 @@ def main():
             cms, cl, _ = ctx.profile(cls)
             if cl:
                 breakdown[cls] = round(cms / prof_steps, 4)
-        traffic = _pmc_traffic(blk_log)
-        if roofline is not None and traffic is not None:
+        traffic, traffic_note = _pmc_traffic(blk_log)
+        if roofline is not None:
             roofline["traffic"] = traffic
+            roofline["traffic_note"] = traffic_note
 
     b_field, b_tree = algorithmic_bytes(log_n, d)
     whole = {"B_alg_bytes": b_field + b_tree, "B_field_bytes": b_field, "B_tree_bytes": b_tree,
@@ -1084,17 +1085,47 @@ def _prover_stage(ctx, fri_amd, with_cpu, log_t=16, log_b=3, queries=3, a1=31415
     return out
 
 
-def _pmc_traffic(log_n):
+SOURCE_GLOBS = ("stark-prover_amd/csrc/*.hip", "stark-prover_amd/csrc/*.hpp", "include/fri_amd.h",
+                "stark-prover_amd/Makefile")
+
+
+def source_hash():
+    """SHA-256 over the library's sources and build flags (the files of
+    SOURCE_GLOBS, sorted by path): what a PMC traffic figure was measured on.
+    tools/pmc_traffic.py stores it beside the figure."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for pat in SOURCE_GLOBS:
+        for path in sorted(glob.glob(os.path.join(ROOT, pat))):
+            h.update(os.path.relpath(path, ROOT).encode() + b"\0")
+            with open(path, "rb") as f:
+                h.update(f.read())
+            h.update(b"\0")
+    return h.hexdigest()
+
+
+def _pmc_traffic(log_n, path=None):
     """HBM bytes per launch of the dominant kernel from the committed
-    rocprofv3 PMC summary (profiles/pmc_traffic.json), if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    rocprofv3 PMC summary (profiles/pmc_traffic.json), and a note.  The
+    figure is used only when it was collected on the library built from the
+    same sources (source_hash); otherwise traffic is null and the note says
+    why: a kernel change must not carry a stale figure."""
+    path = path or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             j = json.load(f)
-        ent = j.get(str(log_n), {}).get(DOMINANT)
-        return ent["hbm_bytes_per_launch"] if ent else None
-    except (OSError, ValueError, KeyError):
-        return None
+        ent = j.get(str(log_n), {})
+        dom = ent.get(DOMINANT)
+        if not dom:
+            return None, f"no PMC figure for 2^{log_n} in profiles/pmc_traffic.json"
+        want = source_hash()
+        if ent.get("source_hash") != want:
+            return None, (f"profiles/pmc_traffic.json was collected on sources {str(ent.get('source_hash'))[:12]}, "
+                          f"this build is {want[:12]}: re-collect (tools/collect_profiles.sh)")
+        return dom["hbm_bytes_per_launch"], f"rocprofv3 PMC FETCH_SIZE + WRITE_SIZE, sources {want[:12]}"
+    except (OSError, ValueError, KeyError) as e:
+        return None, f"profiles/pmc_traffic.json unreadable: {e}"
 
 
 def _single_point(fri_amd, device, log_n, blowup_log, steps):
@@ -1144,7 +1175,10 @@ def _host_info():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count()
-    return {"cpu_model": model, "nproc": avail, "cpu_count": os.cpu_count()}
+    return {"cpu_model": model, "nproc": avail, "sched_getaffinity": avail, "cpu_count": os.cpu_count(),
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
+            "share_rule": "the GPU pool allots 16 host CPUs per GPU and asks jobs to size worker pools to that share "
+                          "(OMP_NUM_THREADS=16 on the box); nproc / os.cpu_count() show the whole machine"}
 
 
 def _median_runs(fn, runs, warmup=1):

@@ -51,3 +51,26 @@ def test_spawn_relays_rank0_line(monkeypatch, capsys):
     assert bench._spawn_ranks(2, []) == 3
     monkeypatch.setattr(bench, "spawn_command", lambda g, a, p: [sys.executable, "-c", "pass"])
     assert bench._spawn_ranks(2, []) == 1                 # no line: a failure, even with status 0
+
+
+def test_pmc_traffic_only_for_the_same_sources(tmp_path):
+    """roofline.traffic comes from profiles/pmc_traffic.json only when the
+    figure was collected on the sources of this build (source_hash)."""
+    ent = {"merkle_layer0_leaf": {"hbm_bytes_per_launch": 1.25e9}}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"24": dict(ent, source_hash=bench.source_hash())}))
+    val, note = bench._pmc_traffic(24, str(p))
+    assert val == 1.25e9 and bench.source_hash()[:12] in note
+    p.write_text(json.dumps({"24": dict(ent, source_hash="0" * 64)}))
+    val, note = bench._pmc_traffic(24, str(p))
+    assert val is None and "re-collect" in note
+    val, note = bench._pmc_traffic(20, str(p))
+    assert val is None
+
+
+def test_source_hash_covers_the_kernels():
+    import glob
+    files = [f for pat in bench.SOURCE_GLOBS for f in glob.glob(os.path.join(ROOT, pat))]
+    names = {os.path.basename(f) for f in files}
+    assert {"fri_layer.hip", "fri_kernels.hip", "fri_api.hip", "sha256_fast.hpp", "fri_amd.h", "Makefile"} <= names
+    assert len(bench.source_hash()) == 64

@@ -43,7 +43,10 @@ def main():
     res = {}
     if os.path.exists(out):
         res = json.load(open(out))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from bench import source_hash          # the sources this library was built from (bench.py checks it)
     res[str(log_n)] = {
+        "source_hash": source_hash(),
         "merkle_layer0_leaf": dict(dom, kernel=dom_name),
         "all_kernels_avg_per_launch": kernels,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (csv), KiB -> bytes, "
