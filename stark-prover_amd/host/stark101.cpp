@@ -194,6 +194,14 @@ Gpu::Gpu(int device, uint32_t log_n_max) : log_n_max_(log_n_max) {
     }
 }
 
+Gpu::Gpu(const std::vector<int>& devices, uint32_t log_n_max, int transport) : log_n_max_(log_n_max) {
+    int rc = fri_ctx_create_multi(devices.data(), static_cast<uint32_t>(devices.size()), log_n_max, transport, &ctx_);
+    if (rc != FRI_OK) {
+        ctx_ = nullptr;
+        throw Panic("fri_ctx_create_multi failed (code " + std::to_string(rc) + ")");
+    }
+}
+
 Gpu::~Gpu() {
     if (ctx_) fri_ctx_destroy(ctx_);
 }

@@ -255,6 +255,12 @@ FE omega(uint32_t log_n);
 class Gpu {
   public:
     Gpu(int device, uint32_t log_n_max);
+    // A team over several GPUs driven from this thread (fri_ctx_create_multi;
+    // a device may repeat; transport FRI_TRANSPORT_NONE = RCCL if it
+    // initialises, else peer).  Every call below takes it unchanged: a
+    // codeword >= 2^20 is committed coset-sharded over the devices by ONE
+    // fri_commit, and the proof's layers and trees serve as on one GPU.
+    Gpu(const std::vector<int>& devices, uint32_t log_n_max, int transport = FRI_TRANSPORT_NONE);
     ~Gpu();
     Gpu(const Gpu&) = delete;
     Gpu& operator=(const Gpu&) = delete;

@@ -451,6 +451,36 @@ TEST(gpu, auth_path_entry_points_agree) {
         ASSERT_EQ(off, plen);
     }
 }
+// The same reference surface on a team context (four ranks on device 0,
+// peer transport): fri_commit_coset, the proof's trees and decommit_fri give
+// the bytes a one-GPU context gives, and verify_fri accepts them.
+TEST(gpu, team_context_matches_single_gpu) {
+    const uint32_t log_n = 21;
+    std::vector<FE> cs;
+    uint64_t x = 4242;
+    for (size_t i = 0; i < (size_t{1} << (log_n - 3)); i++) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        cs.push_back(FE(x >> 33));
+    }
+    auto team = std::make_shared<Gpu>(std::vector<int>{0, 0, 0, 0}, log_n, FRI_TRANSPORT_PEER);
+    auto one = std::make_shared<Gpu>(0, log_n);
+    FriChannel a, b;
+    FRIProof pa = fri_commit_coset(Poly(cs), log_n, FE(5), a, team);
+    FRIProof pb = fri_commit_coset(Poly(cs), log_n, FE(5), b, one);
+    ASSERT_EQ(pa.n_layers(), pb.n_layers());
+    for (size_t k = 0; k < pa.n_layers(); k++) ASSERT_EQ(pa.fri_merkles[k].root(), pb.fri_merkles[k].root());
+    ASSERT_EQ(a.state, b.state);
+    for (size_t idx : {size_t{0}, size_t{777777}, (size_t{1} << log_n) - 1})
+        ASSERT_TRUE(pa.fri_merkles[1].get_authentication_path(idx % (size_t{1} << (log_n - 1))) ==
+                    pb.fri_merkles[1].get_authentication_path(idx % (size_t{1} << (log_n - 1))));
+    const size_t n0 = a.proof.size();
+    decommit_fri(3, (size_t{1} << log_n) - 1, pa, a);
+    decommit_fri(3, (size_t{1} << log_n) - 1, pb, b);
+    ASSERT_EQ(a.state, b.state);
+    ASSERT_TRUE(a.proof == b.proof);
+    ASSERT_TRUE(a.proof.size() > n0);
+    ASSERT_TRUE(verify_fri(a.proof, log_n, pa.n_layers(), 3, (size_t{1} << log_n) - 1));
+}
 TEST(gpu, layers_lde_interpolate_merkle) {
     const GoldenCase* c = nullptr;
     for (const auto& g : GOLDEN)
