@@ -1,0 +1,185 @@
+// Dev microbenchmark: the lane-pair chain node of
+// sha256_quad.hpp with its message schedule W16..W63 made by a second wave.
+//
+// A tree-top level's node is bound by its instruction count on a lone wave
+// (DESIGN.md §6): 1744 instructions per node, 48 x 7 of them the message
+// schedule of the first block.  The schedule depends only on the message,
+// not on the round state, so a producer wave on another SIMD can expand it
+// (plus the round constants: W[t] + K[t]) into LDS while the round wave runs
+// rounds 0..15 on the message words themselves; the round wave then reads
+// the schedule 4 words at a time (ds_read_b128), after one flag check per
+// 16-word block (three per node).
+//
+// One 512-thread workgroup, LEVELS levels of 32 lane-pair nodes on wave 0
+// (node q hashes digests q and (q + 16) mod 32 of the previous level), an
+// LDS-only barrier per level for all eight waves, s_memtime around each
+// level on wave 0 lane 0:
+//   mode 0: shaq::node (the product node), the other waves only pass the barriers
+//   mode 1: producer on wave 1 (SIMD 1), round wave reads the schedule from LDS
+//   mode 2: producer on wave 4 (the round wave's own SIMD): issue contention
+//   mode 3: as mode 1, but the round wave skips the flag checks (the
+//           producer's lead measured without the waits; result unchecked)
+// Every mode's last level must give the same digests as mode 0 (printed).
+//   hipcc -O3 --offload-arch=gfx950 -I../csrc sched_micro.hip -o sched_micro
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include "sha256_quad.hpp"
+using namespace fri;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+constexpr int LEVELS = 24;
+constexpr int NODES = 32;
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+#define bop(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))
+// sha256_quad.hpp's round and schedule step (the header #undefs its own)
+#define MQ_R(kw)                                                                      \
+    {                                                                                 \
+        const uint32_t _S = bop(shaq::rot(x0, R.r1), shaq::rot(x0, R.r2), shaq::rot(x0, R.r3), 0x96); \
+        const uint32_t _sel = bop(x0, x1, R.m, 0x2D);                                 \
+        const uint32_t _F = bop(_sel, x2, x1, 0xCA);                                  \
+        const uint32_t _hk = (x3 + (kw)) & R.me;                                      \
+        const uint32_t _V = _S + _F + _hk;                                            \
+        const uint32_t _Z = bop(R.me, _V, x3, 0xCA);                                  \
+        const uint32_t _n = _V + shaq::swap01(_Z);                                    \
+        x3 = x2; x2 = x1; x1 = x0; x0 = _n;                                           \
+    }
+#define MQ_W(i)                                                                              \
+    {                                                                                        \
+        const uint32_t _x = bop(R.is_a, w[((i) + 1) & 15], w[((i) + 14) & 15], 0xCA);        \
+        const uint32_t _s = bop(shaq::rot(_x, R.q1), shaq::rot(_x, R.q2), _x >> R.q3, 0x96); \
+        w[i] = w[i] + w[((i) + 9) & 15] + _s + shaq::swap01(_s);                            \
+    }
+
+// Producer: this lane pair's node schedule W16..W63 + K into wk[0..47]
+// (node-major, 48 words), flag = base + b after block b's 16 words.
+__device__ __forceinline__ void produce(uint32_t w[16], uint32_t* wk, uint32_t* flag, uint32_t base, bool store,
+                                        bool flag_lane, const shaq::Role& R) {
+#pragma unroll 1
+    for (int b = 0; b < 3; b++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) MQ_W(i);
+        if (store) {
+            uint4* o = reinterpret_cast<uint4*>(wk + 16 * b);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                o[j] = make_uint4(w[4 * j] + shaf::KTAB[16 * (b + 1) + 4 * j], w[4 * j + 1] + shaf::KTAB[16 * (b + 1) + 4 * j + 1],
+                                  w[4 * j + 2] + shaf::KTAB[16 * (b + 1) + 4 * j + 2],
+                                  w[4 * j + 3] + shaf::KTAB[16 * (b + 1) + 4 * j + 3]);
+        }
+        if (flag_lane) __hip_atomic_store(flag, base + b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// Round wave: the first block with the schedule from wk, then the padding block.
+template <bool WAIT>
+__device__ __forceinline__ void node_ext(const uint32_t l[8], const uint32_t r[8], uint32_t out[4], const shaq::Role& R,
+                                         const uint32_t* wk, const uint32_t* flag, uint32_t base) {
+    uint32_t x0 = R.iv[0], x1 = R.iv[1], x2 = R.iv[2], x3 = R.iv[3];
+#pragma unroll
+    for (int i = 0; i < 8; i++) MQ_R(l[i] + shaf::KTAB[i]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) MQ_R(r[i] + shaf::KTAB[8 + i]);
+#pragma unroll 1
+    for (int b = 0; b < 3; b++) {
+        if (WAIT)
+            while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < base + b + 1) {}
+        const uint4* q = reinterpret_cast<const uint4*>(wk + 16 * b);
+        const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        MQ_R(q0.x); MQ_R(q0.y); MQ_R(q0.z); MQ_R(q0.w);
+        MQ_R(q1.x); MQ_R(q1.y); MQ_R(q1.z); MQ_R(q1.w);
+        MQ_R(q2.x); MQ_R(q2.y); MQ_R(q2.z); MQ_R(q2.w);
+        MQ_R(q3.x); MQ_R(q3.y); MQ_R(q3.z); MQ_R(q3.w);
+    }
+    out[0] = R.iv[0] + x0; out[1] = R.iv[1] + x1; out[2] = R.iv[2] + x2; out[3] = R.iv[3] + x3;
+    shaq::compress_kw(out, shaf::PAD_KW_C.kw, R);
+}
+
+__global__ __launch_bounds__(512) void k_sched(const uint32_t* in, uint32_t* out, unsigned long long* clk, int mode) {
+    __shared__ uint4 lds[2 * 2 * NODES];                 // A, B: 32 digests each (2 x uint4)
+    __shared__ __attribute__((aligned(16))) uint32_t wk[NODES * 48];
+    __shared__ uint32_t flag;
+    uint4* A = lds;
+    uint4* B = lds + 2 * NODES;
+    const uint32_t tid = threadIdx.x;
+    if (tid < 2 * NODES) A[tid] = reinterpret_cast<const uint4*>(in)[tid];
+    if (tid == 0) flag = 0;
+    __syncthreads();
+    const shaq::Role R = shaq::role_of(tid);
+    const uint32_t prod_wave = mode == 2 ? 4u : 1u;
+    const bool round_wave = tid < 64;
+    const bool prod = mode >= 1 && (tid >> 6) == prod_wave;
+    uint4* a = A;
+    uint4* b = B;
+    for (int it = 0; it < LEVELS; it++) {
+        const uint32_t base = 3u * (uint32_t)it;
+        if (round_wave || prod) {
+            const uint32_t lane = tid & 63, q = lane >> 1, half = (lane & 1u) ^ 1u;
+            const uint32_t li = 2 * q, ri = 2 * ((q + 16) & 31);
+            const uint4 l0 = a[li], l1 = a[li + 1], r0 = a[ri], r1 = a[ri + 1];
+            uint32_t l[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+            uint32_t r[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+            if (prod) {
+                uint32_t w[16];
+#pragma unroll
+                for (int i = 0; i < 8; i++) { w[i] = l[i]; w[8 + i] = r[i]; }
+                produce(w, wk + 48 * q, &flag, base, (lane & 1u) == 0, lane == 0, R);
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+                uint32_t o[4];
+                if (mode == 0) shaq::node(l, r, o, R);
+                else if (mode == 3) node_ext<false>(l, r, o, R, wk + 48 * q, &flag, base);
+                else node_ext<true>(l, r, o, R, wk + 48 * q, &flag, base);
+                const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+                b[2 * q + half] = make_uint4(o[0], o[1], o[2], o[3]);
+                if (tid == 0) clk[it] = c1 - c0;
+            }
+        }
+        lds_barrier();
+        uint4* t = a; a = b; b = t;
+    }
+    if (tid < 2 * NODES) reinterpret_cast<uint4*>(out)[tid] = a[tid];
+}
+
+int main() {
+    uint32_t h_in[NODES * 8];
+    for (int i = 0; i < NODES * 8; i++) h_in[i] = 0x9e3779b9u * (i + 1) ^ (i << 9);
+    uint32_t *d_in, *d_out;
+    unsigned long long* d_clk;
+    CK(hipMalloc(&d_in, sizeof(h_in)));
+    CK(hipMalloc(&d_out, sizeof(h_in)));
+    CK(hipMalloc(&d_clk, LEVELS * 8));
+    CK(hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice));
+    uint32_t ref[NODES * 8];
+    const char* names[4] = {"product node (schedule in the round wave)", "producer wave 1 (SIMD 1)",
+                            "producer wave 4 (same SIMD)", "producer wave 1, no flag waits"};
+    for (int mode = 0; mode < 4; mode++) {
+        double sum = 0;
+        int n = 0;
+        bool same = true;
+        printf("mode %d: %s\n", mode, names[mode]);
+        for (int rep = 0; rep < 8; rep++) {
+            hipLaunchKernelGGL(k_sched, dim3(1), dim3(512), 0, 0, d_in, d_out, d_clk, mode);
+            CK(hipDeviceSynchronize());
+            unsigned long long c[LEVELS];
+            uint32_t o[NODES * 8];
+            CK(hipMemcpy(c, d_clk, sizeof(c), hipMemcpyDeviceToHost));
+            CK(hipMemcpy(o, d_out, sizeof(o), hipMemcpyDeviceToHost));
+            if (mode == 0 && rep == 0) memcpy(ref, o, sizeof(o));
+            same = same && memcmp(ref, o, sizeof(o)) == 0;
+            printf("  ");
+            for (int i = 0; i < LEVELS; i++) printf("%.2f ", c[i] / 1000.0);
+            printf("\n");
+            if (rep > 0)
+                for (int i = 2; i < LEVELS; i++) { sum += c[i]; n++; }
+        }
+        printf("  mean level (K cycles, reps 1-7, levels 2-23): %.3f   digests equal to mode 0: %s\n", sum / n / 1000.0,
+               same ? "yes" : "NO");
+    }
+    return 0;
+}
