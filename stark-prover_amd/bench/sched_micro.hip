@@ -19,6 +19,8 @@
 //   mode 2: producer on wave 4 (the round wave's own SIMD): issue contention
 //   mode 3: as mode 1, but the round wave skips the flag checks (the
 //           producer's lead measured without the waits; result unchecked)
+//   mode 4: as mode 1, the round wave prefetching each block's flag and
+//           words during the previous block's rounds (node_pre)
 // Every mode's last level must give the same digests as mode 0 (printed).
 //   hipcc -O3 --offload-arch=gfx950 -I../csrc sched_micro.hip -o sched_micro
 #include <hip/hip_runtime.h>
@@ -48,37 +50,14 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
         const uint32_t _n = _V + shaq::swap01(_Z);                                    \
         x3 = x2; x2 = x1; x1 = x0; x0 = _n;                                           \
     }
-#define MQ_W(i)                                                                              \
-    {                                                                                        \
-        const uint32_t _x = bop(R.is_a, w[((i) + 1) & 15], w[((i) + 14) & 15], 0xCA);        \
-        const uint32_t _s = bop(shaq::rot(_x, R.q1), shaq::rot(_x, R.q2), _x >> R.q3, 0x96); \
-        w[i] = w[i] + w[((i) + 9) & 15] + _s + shaq::swap01(_s);                            \
-    }
+// produce / node_ext: the product code (sha256_quad.hpp); node_pre below is
+// the prefetching variant that measured slower (mode 4).
+using shaq::node_ext;
+using shaq::produce;
 
-// Producer: this lane pair's node schedule W16..W63 + K into wk[0..47]
-// (node-major, 48 words), flag = base + b after block b's 16 words.
-__device__ __forceinline__ void produce(uint32_t w[16], uint32_t* wk, uint32_t* flag, uint32_t base, bool store,
-                                        bool flag_lane, const shaq::Role& R) {
-#pragma unroll 1
-    for (int b = 0; b < 3; b++) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) MQ_W(i);
-        if (store) {
-            uint4* o = reinterpret_cast<uint4*>(wk + 16 * b);
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                o[j] = make_uint4(w[4 * j] + shaf::KTAB[16 * (b + 1) + 4 * j], w[4 * j + 1] + shaf::KTAB[16 * (b + 1) + 4 * j + 1],
-                                  w[4 * j + 2] + shaf::KTAB[16 * (b + 1) + 4 * j + 2],
-                                  w[4 * j + 3] + shaf::KTAB[16 * (b + 1) + 4 * j + 3]);
-        }
-        if (flag_lane) __hip_atomic_store(flag, base + b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-}
-
-// Round wave: the first block with the schedule from wk, then the padding block.
-template <bool WAIT>
-__device__ __forceinline__ void node_ext(const uint32_t l[8], const uint32_t r[8], uint32_t out[4], const shaq::Role& R,
-                                         const uint32_t* wk, const uint32_t* flag, uint32_t base) {
+// mode 3: the schedule read without any flag check (unsynchronised: timing only)
+__device__ __forceinline__ void node_nowait(const uint32_t l[8], const uint32_t r[8], uint32_t out[4],
+                                            const shaq::Role& R, const uint32_t* wk) {
     uint32_t x0 = R.iv[0], x1 = R.iv[1], x2 = R.iv[2], x3 = R.iv[3];
 #pragma unroll
     for (int i = 0; i < 8; i++) MQ_R(l[i] + shaf::KTAB[i]);
@@ -86,14 +65,53 @@ __device__ __forceinline__ void node_ext(const uint32_t l[8], const uint32_t r[8
     for (int i = 0; i < 8; i++) MQ_R(r[i] + shaf::KTAB[8 + i]);
 #pragma unroll 1
     for (int b = 0; b < 3; b++) {
-        if (WAIT)
-            while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < base + b + 1) {}
         const uint4* q = reinterpret_cast<const uint4*>(wk + 16 * b);
         const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
         MQ_R(q0.x); MQ_R(q0.y); MQ_R(q0.z); MQ_R(q0.w);
         MQ_R(q1.x); MQ_R(q1.y); MQ_R(q1.z); MQ_R(q1.w);
         MQ_R(q2.x); MQ_R(q2.y); MQ_R(q2.z); MQ_R(q2.w);
         MQ_R(q3.x); MQ_R(q3.y); MQ_R(q3.z); MQ_R(q3.w);
+    }
+    out[0] = R.iv[0] + x0; out[1] = R.iv[1] + x1; out[2] = R.iv[2] + x2; out[3] = R.iv[3] + x3;
+    shaq::compress_kw(out, shaf::PAD_KW_C.kw, R);
+}
+
+// Round wave, prefetching: block b+1's flag and schedule words are read while
+// block b's rounds run (relaxed flag load, then the data loads in program
+// order: LDS executes a wave's operations in order, so data read after a flag
+// that shows the block complete is that block's).  Only if the flag was not
+// set yet does the wave wait and read the block again.
+__device__ __forceinline__ uint32_t flag_relaxed(const uint32_t* f) {
+    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void node_pre(const uint32_t l[8], const uint32_t r[8], uint32_t out[4], const shaq::Role& R,
+                                         const uint32_t* wk, const uint32_t* flag, uint32_t base) {
+    uint32_t x0 = R.iv[0], x1 = R.iv[1], x2 = R.iv[2], x3 = R.iv[3];
+#pragma unroll
+    for (int i = 0; i < 8; i++) MQ_R(l[i] + shaf::KTAB[i]);
+    const uint4* q = reinterpret_cast<const uint4*>(wk);
+    uint32_t f = flag_relaxed(flag);
+    asm volatile("" ::: "memory");
+    uint4 c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3];
+#pragma unroll
+    for (int i = 0; i < 8; i++) MQ_R(r[i] + shaf::KTAB[8 + i]);
+#pragma unroll 1
+    for (int b = 0; b < 3; b++) {
+        if (f < base + b + 1) {                         // not ready when prefetched: wait, read again
+            while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < base + b + 1) {}
+            c0 = q[4 * b]; c1 = q[4 * b + 1]; c2 = q[4 * b + 2]; c3 = q[4 * b + 3];
+        }
+        uint4 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
+        if (b < 2) {
+            f = flag_relaxed(flag);
+            asm volatile("" ::: "memory");
+            n0 = q[4 * b + 4]; n1 = q[4 * b + 5]; n2 = q[4 * b + 6]; n3 = q[4 * b + 7];
+        }
+        MQ_R(c0.x); MQ_R(c0.y); MQ_R(c0.z); MQ_R(c0.w);
+        MQ_R(c1.x); MQ_R(c1.y); MQ_R(c1.z); MQ_R(c1.w);
+        MQ_R(c2.x); MQ_R(c2.y); MQ_R(c2.z); MQ_R(c2.w);
+        MQ_R(c3.x); MQ_R(c3.y); MQ_R(c3.z); MQ_R(c3.w);
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
     }
     out[0] = R.iv[0] + x0; out[1] = R.iv[1] + x1; out[2] = R.iv[2] + x2; out[3] = R.iv[3] + x3;
     shaq::compress_kw(out, shaf::PAD_KW_C.kw, R);
@@ -133,8 +151,9 @@ __global__ __launch_bounds__(512) void k_sched(const uint32_t* in, uint32_t* out
                 const unsigned long long c0 = __builtin_amdgcn_s_memtime();
                 uint32_t o[4];
                 if (mode == 0) shaq::node(l, r, o, R);
-                else if (mode == 3) node_ext<false>(l, r, o, R, wk + 48 * q, &flag, base);
-                else node_ext<true>(l, r, o, R, wk + 48 * q, &flag, base);
+                else if (mode == 3) node_nowait(l, r, o, R, wk + 48 * q);
+                else if (mode == 4) node_pre(l, r, o, R, wk + 48 * q, &flag, base);
+                else node_ext(l, r, o, R, wk + 48 * q, &flag, base);
                 const unsigned long long c1 = __builtin_amdgcn_s_memtime();
                 b[2 * q + half] = make_uint4(o[0], o[1], o[2], o[3]);
                 if (tid == 0) clk[it] = c1 - c0;
@@ -156,9 +175,10 @@ int main() {
     CK(hipMalloc(&d_clk, LEVELS * 8));
     CK(hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice));
     uint32_t ref[NODES * 8];
-    const char* names[4] = {"product node (schedule in the round wave)", "producer wave 1 (SIMD 1)",
-                            "producer wave 4 (same SIMD)", "producer wave 1, no flag waits"};
-    for (int mode = 0; mode < 4; mode++) {
+    const char* names[5] = {"product node (schedule in the round wave)", "producer wave 1 (SIMD 1)",
+                            "producer wave 4 (same SIMD)", "producer wave 1, no flag waits",
+                            "producer wave 1, round wave prefetches the next block"};
+    for (int mode = 0; mode < 5; mode++) {
         double sum = 0;
         int n = 0;
         bool same = true;

@@ -113,6 +113,51 @@ __device__ __forceinline__ void pair_level(const uint4* A, uint4* B, uint32_t* o
     reinterpret_cast<uint4*>(out + 8 * q)[half] = v;
 }
 
+// Narrow levels (<= 32 nodes, one round wave) with the message schedule made
+// by wave 1 of the workgroup (sha256_quad.hpp produce / node_ext): the round
+// wave, wave 0, issues 48 x 7 fewer instructions per node.  Wave 1 sits on
+// another SIMD (waves are dealt to the SIMDs in turn), and at these levels it
+// is otherwise idle.  `ord`: the level's ordinal within the launch, strictly
+// increasing (the flag counts 3 per level).  0 = off (A/B builds).
+#ifndef FRI_SCHED_PRODUCER
+#define FRI_SCHED_PRODUCER 1
+#endif
+struct SchedLds {
+    uint32_t wk[32 * 48];       // per node W16..W63 + K (16-byte aligned rows of 48 words)
+    uint32_t flag;
+};
+__device__ __forceinline__ void sched_init(SchedLds* sl) {
+    if (FRI_SCHED_PRODUCER && threadIdx.x == 0) sl->flag = 0u;    // (before the launch's first barrier)
+}
+__device__ __forceinline__ void pair_level_s(const uint4* A, uint4* B, uint32_t* out, uint32_t tid, uint32_t cnt,
+                                             const shaq::Role& R, SchedLds* sl, uint32_t ord) {
+    if (!FRI_SCHED_PRODUCER || cnt > 32) {
+        pair_level(A, B, out, tid, cnt, R);
+        return;
+    }
+    const uint32_t wv = tid >> 6;
+    if (wv > 1) return;
+    const uint32_t lane = tid & 63u;
+    const uint32_t q = (lane >> 1) & (cnt - 1), half = (lane & 1u) ^ 1u;
+    const bool real = lane < 2 * cnt;            // spare lanes redo node q mod cnt and store nothing (see pair_level)
+    Dg a, b;
+    dg_lds_load(A + 4 * q, a);
+    dg_lds_load(A + 4 * q + 2, b);
+    if (wv == 1) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 8; i++) { w[i] = a.w[i]; w[8 + i] = b.w[i]; }
+        shaq::produce(w, sl->wk + 48 * q, &sl->flag, 3u * ord, real && (lane & 1u) == 0u, lane == 0u, R);
+        return;
+    }
+    uint32_t o[4];
+    shaq::node_ext(a.w, b.w, o, R, sl->wk + 48 * q, &sl->flag, 3u * ord);
+    if (!real) return;
+    const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
+    B[2 * q + half] = v;
+    reinterpret_cast<uint4*>(out + 8 * q)[half] = v;
+}
+
 // Barrier that waits only for this wave's LDS traffic: HIP's __syncthreads()
 // also drains vmcnt, i.e. waits ~1 us for the level's global digest stores,
 // which no other wave of the workgroup reads.
@@ -294,6 +339,8 @@ __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
     if (gated_off(t)) return;
     __shared__ uint4 lds[2 * 256 + 2 * 128];
     __shared__ int32_t red[12];
+    __shared__ SchedLds sl;
+    sched_init(&sl);
     const uint32_t L = t.L;
     const size_t wg = PAIR ? (size_t)blockIdx.x + t.wg_base : (size_t)blockIdx.x;
     const size_t grid = PAIR ? (size_t)t.wg_total : (size_t)gridDim.x;   // the whole layer's workgroups
@@ -325,7 +372,7 @@ __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
         cnt >>= 1;
         uint32_t* out = tr + 8 * (level_offset(L, j) + (wg << (8 - j)));
         if ((size_t)cnt * grid < WIDE_PAIR_MAX) {
-            pair_level(A, B, out, threadIdx.x, cnt, qr);   // latency-bound level: node per lane pair
+            pair_level_s(A, B, out, threadIdx.x, cnt, qr, &sl, j);   // latency-bound level: node per lane pair
         } else if (threadIdx.x < cnt) {
             Dg a, b, o;
             dg_lds_load(A + 4 * threadIdx.x, a);
@@ -366,6 +413,8 @@ __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L
     // thread), so LDS holds only levels 1.. (NIN/2 + NIN/4 digests): more
     // workgroups per CU for the wide instance
     __shared__ uint4 lds[NIN + NIN / 2];
+    __shared__ SchedLds sl;
+    sched_init(&sl);
     uint4* A = lds;
     uint4* B = lds + NIN;
     const uint32_t t = threadIdx.x;
@@ -393,7 +442,7 @@ __global__ __launch_bounds__(NIN / 2) void k_tree_mid(uint32_t* tree, uint32_t L
         const bool narrow = NIN == 1024 && !MID_PAIR_BY_WG ? (size_t)cnt * gridDim.x < WIDE_PAIR_MAX
                                                            : 2 * cnt <= NIN / 2;
         if (narrow) {
-            pair_level(A, B, out, t, cnt, qr);         // narrow: latency-bound
+            pair_level_s(A, B, out, t, cnt, qr, &sl, j);   // narrow: latency-bound
         } else if (t < cnt) {
             Dg a, b, o;
             dg_lds_load(A + 4 * t, a);
@@ -417,6 +466,8 @@ __global__ __launch_bounds__(256) void k_tree_mid8(uint32_t* tree, uint32_t L, u
     if (st && gate >= 0 && !st->active[gate]) return;
     chain_prio();
     __shared__ uint4 lds[256 + 128];
+    __shared__ SchedLds sl;
+    sched_init(&sl);
     uint4* A = lds;
     uint4* B = lds + 256;
     const uint32_t t = threadIdx.x;
@@ -440,7 +491,7 @@ __global__ __launch_bounds__(256) void k_tree_mid8(uint32_t* tree, uint32_t L, u
 #pragma unroll 1
     for (uint32_t j = 2; j <= 8; j++) {
         cnt >>= 1;
-        pair_level(A, B, tree + 8 * (level_offset(L, l + j) + (base >> j)), t, cnt, qr);
+        pair_level_s(A, B, tree + 8 * (level_offset(L, l + j) + (base >> j)), t, cnt, qr, &sl, j);
         lds_barrier();
         uint4* tmp = A; A = B; B = tmp;
     }
@@ -585,6 +636,8 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     chain_prio();
     __shared__ uint4 lds[2 * 1024 + 2 * 512];
     __shared__ int32_t red[24];
+    __shared__ SchedLds sl;
+    sched_init(&sl);
     const uint32_t L = t.L;
     const uint32_t N = 1u << (L - l);
     const uint32_t tid = threadIdx.x;
@@ -712,7 +765,7 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
 #ifdef FRI_STAMPS
                 if (it < 18 && tid == 0) TOP_CLK(24 + 2 * it);
 #endif
-                pair_level(A, B, out, tid, cnt, R);
+                pair_level_s(A, B, out, tid, cnt, R, &sl, it);
 #ifdef FRI_STAMPS
                 if (it < 18 && tid == 0) TOP_CLK(25 + 2 * it);
 #endif
@@ -824,6 +877,9 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
     __shared__ uint32_t s_beta_m, s_active;
     __shared__ int32_t s_deg;
     __shared__ uint32_t s_fbeta[TAIL_LOG + 2];   // the test hook's betas of these layers (0: not forced)
+    __shared__ SchedLds sl;
+    sched_init(&sl);
+    uint32_t ord = 0;                            // narrow levels so far (schedule producer flag)
     const uint32_t tid = threadIdx.x;
     const bool chan_wave = tid >= 448;
     DevState* st = t0.st;
@@ -931,7 +987,7 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
                 cnt >>= 1;
                 uint32_t* out = tr + 8 * level_offset(L, 1 + it);
                 if (cnt <= 128) {
-                    pair_level(A, B, out, tid, cnt, R);
+                    pair_level_s(A, B, out, tid, cnt, R, &sl, ord++);
                 } else {
 #pragma unroll 1
                     for (uint32_t q = tid; q < cnt; q += blockDim.x) {

@@ -115,6 +115,64 @@ __device__ __forceinline__ void compress_kw(uint32_t st[4], const uint32_t* kw, 
     }
     st[0] += x0; st[1] += x1; st[2] += x2; st[3] += x3;
 }
+// ---- schedule producer (stark-prover_amd/bench/sched_micro.hip)
+// The first block's message schedule W16..W63 depends only on the message,
+// not on the round state, so a second wave of the workgroup, on another
+// SIMD, expands it (with the round constants: W[t] + K[t]) into LDS while the
+// round wave runs rounds 0..15 on the message words; the round wave reads it
+// 4 words at a time after one flag check per 16-word block.  The round wave
+// issues 48 x 7 fewer instructions per node: 8.51 -> 7.51 K cycles per
+// dependent node in the micro (profiles/r05_sched_micro.txt).  A producer on
+// the round wave's own SIMD is slower than none (9.09 K): the two waves then
+// share one issue port.
+//
+// Producer: the node's schedule into wk[0..47] (48 words, 16-byte aligned),
+// flag = base + b + 1 once block b's 16 words are stored.  Both lanes of a
+// pair run (the split schedule needs the pair); `store` on one lane of it.
+__device__ __forceinline__ void produce(uint32_t w[16], uint32_t* wk, uint32_t* flag, uint32_t base, bool store,
+                                        bool flag_lane, const Role& R) {
+#pragma unroll 1
+    for (int b = 0; b < 3; b++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) SHAQ_W(i);
+        if (store) {
+            uint4* o = reinterpret_cast<uint4*>(wk + 16 * b);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                o[j] = make_uint4(w[4 * j] + shaf::KTAB[16 * (b + 1) + 4 * j],
+                                  w[4 * j + 1] + shaf::KTAB[16 * (b + 1) + 4 * j + 1],
+                                  w[4 * j + 2] + shaf::KTAB[16 * (b + 1) + 4 * j + 2],
+                                  w[4 * j + 3] + shaf::KTAB[16 * (b + 1) + 4 * j + 3]);
+        }
+        // (release: the wave's schedule stores are complete before the flag)
+        if (flag_lane) __hip_atomic_store(flag, base + b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// Round wave: node SHA256(l || r) with the first block's rounds 16..63 fed
+// from wk (W + K, written by produce), then the padding block.  Same digest
+// halves as node().
+__device__ __forceinline__ void node_ext(const uint32_t l[8], const uint32_t r[8], uint32_t out[4], const Role& R,
+                                         const uint32_t* wk, const uint32_t* flag, uint32_t base) {
+    uint32_t x0 = R.iv[0], x1 = R.iv[1], x2 = R.iv[2], x3 = R.iv[3];
+#pragma unroll
+    for (int i = 0; i < 8; i++) SHAQ_R(l[i] + shaf::KTAB[i]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) SHAQ_R(r[i] + shaf::KTAB[8 + i]);
+#pragma unroll 1
+    for (int b = 0; b < 3; b++) {
+        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < base + b + 1) {}
+        const uint4* q = reinterpret_cast<const uint4*>(wk + 16 * b);
+        const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        SHAQ_R(q0.x); SHAQ_R(q0.y); SHAQ_R(q0.z); SHAQ_R(q0.w);
+        SHAQ_R(q1.x); SHAQ_R(q1.y); SHAQ_R(q1.z); SHAQ_R(q1.w);
+        SHAQ_R(q2.x); SHAQ_R(q2.y); SHAQ_R(q2.z); SHAQ_R(q2.w);
+        SHAQ_R(q3.x); SHAQ_R(q3.y); SHAQ_R(q3.z); SHAQ_R(q3.w);
+    }
+    out[0] = R.iv[0] + x0; out[1] = R.iv[1] + x1; out[2] = R.iv[2] + x2; out[3] = R.iv[3] + x3;
+    compress_kw(out, shaf::PAD_KW_C.kw, R);
+}
+
 #undef SHAQ_R
 #undef SHAQ_W
 #undef bop
