@@ -423,6 +423,9 @@ int fri_reset_profile(fri_ctx* ctx);
  * twiddles, scratch, the commit plan (layers, trees, x^-1 tables), multi-GPU
  * buffers and any grown scratch.  (Diagnostic; no reference counterpart.) */
 int fri_ctx_device_bytes(fri_ctx* ctx, uint64_t* current, uint64_t* peak);
+/* Test hook: the context's device allocations fail (FRI_ENOMEM paths) once
+ * they would take it past cap_bytes of HBM (0: no cap). */
+int fri_debug_set_device_cap(fri_ctx* ctx, uint64_t cap_bytes);
 /* Diagnostic build only (-DFRI_STAMPS): top-kernel phase timestamps of the
  * last commit, (FRI_MAX_LAYERS x 24) u64 ticks of the 100 MHz clock.
  * Returns FRI_ESTATE in the product build. */

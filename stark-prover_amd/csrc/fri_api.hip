@@ -230,6 +230,7 @@ struct fri_ctx {
     uint32_t* stall_flag_dev = nullptr;
     std::map<const void*, size_t> allocs;   // device allocations owned by the context (fri_ctx_device_bytes)
     size_t dev_bytes = 0, dev_peak = 0;
+    size_t dev_cap = 0;             // fri_debug_set_device_cap: allocations beyond it fail (0: none)
     Team* team_root = nullptr;      // fri_ctx_create_multi: this context is rank 0 and owns the team
 };
 
@@ -238,6 +239,7 @@ struct fri_ctx {
 template <class T>
 static hipError_t dalloc(fri_ctx* ctx, T** p, size_t bytes) {
     void* q = nullptr;
+    if (ctx->dev_cap && ctx->dev_bytes + bytes > ctx->dev_cap) { *p = nullptr; return hipErrorOutOfMemory; }
     const hipError_t e = hipMalloc(&q, bytes);
     if (e != hipSuccess) { *p = nullptr; return e; }
     *p = static_cast<T*>(q);
@@ -1770,6 +1772,12 @@ extern "C" int fri_debug_plan_layout(size_t d, uint32_t log_n, uint32_t world, u
     }
     return FRI_OK;
 }
+extern "C" int fri_debug_set_device_cap(fri_ctx* ctx, uint64_t cap_bytes) {
+    if (!ctx) return FRI_EINVAL;
+    ctx->dev_cap = (size_t)cap_bytes;
+    return FRI_OK;
+}
+
 extern "C" int fri_ctx_device_bytes(fri_ctx* ctx, uint64_t* current, uint64_t* peak) {
     if (!ctx || !current || !peak) return fail(ctx, FRI_EINVAL, "null argument");
     *current = ctx->dev_bytes;

@@ -135,6 +135,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_debug_attach_loopback": (i32, [vp, i32, i32]),
         "fri_debug_plan_layout": (i32, [sz, u32, u32, u32, ctypes.POINTER(ctypes.c_uint64), sz]),
         "fri_ctx_device_bytes": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+        "fri_debug_set_device_cap": (i32, [vp, ctypes.c_uint64]),
         "fri_debug_stamps": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), sz]),
         "fri_dist_unique_id": (i32, [ctypes.c_char_p]),
         "fri_dist_attach_rccl": (i32, [vp, i32, i32, ctypes.c_char_p]),
@@ -600,6 +601,11 @@ class Context:
 
     def reset_profile(self):
         self._check(self.lib.fri_reset_profile(self.h))
+
+    def set_device_cap(self, cap_bytes: int):
+        """Test hook (fri_debug_set_device_cap): device allocations of this
+        context beyond cap_bytes fail as out-of-memory; 0 removes the cap."""
+        self._check(self.lib.fri_debug_set_device_cap(self.h, cap_bytes))
 
     def device_bytes(self):
         """(current, peak) HBM bytes held by this context (fri_ctx_device_bytes)."""

@@ -484,3 +484,41 @@ def test_rejected_sync_commit_keeps_pending_lane_commit_resident(pctx, oracle, o
         assert int(val) == int(lay[7])
     assert _transcript(pctx.commit_wait(t0)) == oracle_commit(LOG_N, s0)
     assert _transcript(pctx.commit_wait(t1)) == oracle_commit(LOG_N, s1)
+
+
+def test_lane_without_memory_falls_back_and_keeps_input_buffer(oracle, oracle_commit, torch):
+    """A lane that gets no HBM for its plan (a device-memory cap on the
+    context) drops out of the rotation: the commits run on lane 0, lane 0's
+    plan and the input buffer fri_ctx_input_buffer handed out stay valid (only
+    the partial plan is released), and every transcript is right.  Lifting the
+    cap and setting the lanes again brings the lanes back."""
+    import fri_amd
+    d = (1 << LOG_N) >> 3
+    c0 = oracle.splitmix64_np(1201, d).astype(np.uint32)
+    polys = _polys(oracle, torch, [1202, 1203, 1204])
+    cx = fri_amd.Context(0, LOG_N)
+    try:
+        cx.commit(c0, LOG_N)
+        p0 = ctypes.c_void_p()
+        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p0)))
+        cur = cx.device_bytes()[0]
+        cx.set_device_cap(cur + (1 << 16))                   # lane state yes, a second plan no
+        cx.set_lanes(3)
+        ts = [(s, cx.commit_device_async(b.data_ptr(), d, LOG_N)) for s, b in polys]
+        assert [cx.ticket_lane(t) for _, t in ts] == [0, 0, 0]
+        for s, t in ts:
+            assert _transcript(cx.commit_wait(t)) == oracle_commit(LOG_N, s)
+        p1 = ctypes.c_void_p()
+        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p1)))
+        assert p1.value == p0.value
+        cx.commit(c0, LOG_N)                                  # the input buffer holds c0 again
+        t = cx.commit_device_async(p0.value, d, LOG_N)
+        assert _transcript(cx.commit_wait(t)) == oracle_commit(LOG_N, 1201)
+        cx.set_device_cap(0)
+        cx.set_lanes(3)
+        ts = [(s, cx.commit_device_async(b.data_ptr(), d, LOG_N)) for s, b in polys]
+        assert sorted(cx.ticket_lane(t) for _, t in ts) == [0, 1, 2]
+        for s, t in ts:
+            assert _transcript(cx.commit_wait(t)) == oracle_commit(LOG_N, s)
+    finally:
+        cx.close()
