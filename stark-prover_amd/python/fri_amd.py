@@ -614,6 +614,68 @@ class Context:
         return cur.value, peak.value
 
 
+_HIP = None
+
+
+def hip_runtime() -> ctypes.CDLL:
+    """The HIP runtime libfri_amd.so is linked against (loaded with it): for
+    a caller's own device buffers without a second runtime in the process
+    (PyTorch bundles its own libamdhip64)."""
+    global _HIP
+    if _HIP is not None:
+        return _HIP
+    load_library()
+    path = "libamdhip64.so.7"
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64.so" in line and "/torch/" not in line:
+                    path = line.split()[-1]
+                    break
+    except OSError:
+        pass
+    hip = ctypes.CDLL(path)
+    vp = ctypes.c_void_p
+    hip.hipMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t]
+    hip.hipFree.argtypes = [vp]
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(vp)]
+    hip.hipStreamDestroy.argtypes = [vp]
+    hip.hipStreamSynchronize.argtypes = [vp]
+    hip.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
+    _HIP = hip
+    return hip
+
+
+class DeviceBuffer:
+    """A device copy of a uint32 array for fri_commit_device /
+    fri_commit_device_async (hipMalloc, then an upload on a stream of its own,
+    so the null stream never takes one of the process's hardware queues);
+    freed with the object.  ``data_ptr()`` is the device pointer."""
+
+    def __init__(self, arr):
+        a = np.ascontiguousarray(arr, dtype=np.uint32)
+        hip = hip_runtime()
+        self._hip = hip
+        p = ctypes.c_void_p()
+        if hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(max(4, a.nbytes))) != 0:
+            raise FriError(FRI_ENOMEM, "hipMalloc of a device buffer failed")
+        self.ptr = p.value
+        st = ctypes.c_void_p()
+        if (hip.hipStreamCreate(ctypes.byref(st)) != 0 or
+                hip.hipMemcpyAsync(p, a.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(a.nbytes), 1, st) != 0 or
+                hip.hipStreamSynchronize(st) != 0):
+            raise FriError(FRI_EHIP, "upload of a device buffer failed")
+        hip.hipStreamDestroy(st)
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._hip.hipFree(self.ptr)
+            self.ptr = None
+
+
 def plan_layout(d: int, log_n: int, world: int = 1, rank: int = 0) -> dict:
     """The commit plan's layout (fri_debug_plan_layout; host only, no GPU):
     rounds bound, last sharded layer, per-layer slot sizes, x^-1 slices and

@@ -70,3 +70,4 @@ def oracle_commit(corc):
                 "final_value": int(r.final_value), "final_degree": int(r.final_degree),
                 "state": och.state.decode()}
     return run
+

@@ -15,8 +15,10 @@ LOG_N = 16
 
 
 def _dev(torch, coeffs_u32):
-    """A device copy of the coefficients (torch owns the buffer)."""
-    return torch.from_numpy(coeffs_u32.view(np.int32).copy()).cuda()
+    """A device copy of the coefficients, through the library's own HIP
+    runtime (fri_amd.DeviceBuffer; `torch` is unused, kept for the call sites)."""
+    import fri_amd
+    return fri_amd.DeviceBuffer(coeffs_u32)
 
 
 def _transcript(res):
@@ -28,8 +30,9 @@ def _transcript(res):
 
 @pytest.fixture(scope="module")
 def torch():
-    import torch as t
-    return t
+    """(Formerly torch, for device buffers; the buffers now come from the
+    library's own HIP runtime: fri_amd.DeviceBuffer.)"""
+    return None
 
 
 @pytest.fixture()

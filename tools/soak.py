@@ -129,7 +129,6 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--contexts", type=int, default=1)
     a = ap.parse_args(argv)
-    import torch
     import fri_amd
     import fri_oracle as fo
     corc = fo.load_c_oracle()
@@ -139,7 +138,7 @@ def main(argv=None):
         d = (1 << L) >> 3
         for j in range(4):
             c = fo.splitmix64_np(7000 + 10 * L + j, d).astype(np.uint32)
-            dev = torch.from_numpy(c.view(np.int32).copy()).cuda()
+            dev = fri_amd.DeviceBuffer(c)        # the library's own HIP runtime (no torch)
             polys[(L, j)] = (c, dev, oracle_transcript(corc, fo, c, L))
     cx = [Driven(fri_amd, polys, rng) for _ in range(a.contexts)]
     kinds = {}
