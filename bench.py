@@ -676,8 +676,8 @@ def main():
             if team_n:
                 nd = len(set(team_devices or []))
                 par = (f"coset-sharded x{n_ranks} in ONE process (team context, peer transport: each collective "
-                       f"one pull kernel over xGMI) on {nd} distinct device(s); the other ranks copy rank 0's "
-                       f"input buffer inside every step")
+                       f"one pull kernel over xGMI) on {nd} distinct device(s); inputs resident on every rank "
+                       f"(FRI_FLAG_RANK_INPUTS)")
                 if fallback:
                     par += f" (FALLBACK: {fallback})"
             else:
@@ -764,9 +764,11 @@ def _team_stage(fri_amd, devices, points, args, timed):
     """The coset-sharded commit over `devices` from THIS process: one team
     context (fri_ctx_create_multi, peer transport), one fri_commit_device
     call per step (the single-call surface of fri_commit.rs:72-76).  Inputs
-    resident: rank 0's input buffer, which the other ranks copy over xGMI
-    inside every step.  Each point's first transcript is checked against the
-    C oracle's golden transcript; a mismatch raises."""
+    resident on every rank, as in the one-process-per-GPU run: the first
+    (checked) commit stages the coefficients into every rank's input buffer
+    and the timed steps pass FRI_FLAG_RANK_INPUTS.  Each point's first
+    transcript is checked against the C oracle's golden transcript; a
+    mismatch raises."""
     G = len(devices)
     logG = G.bit_length() - 1
     ctx = fri_amd.Context.multi(devices, max(L for _, L in points), transport="peer")
@@ -787,8 +789,8 @@ def _team_stage(fri_amd, devices, points, args, timed):
         res = fri_amd.CommitResult()
 
         def step(dptr=dptr, dL=dL, L=L, res=res):
-            ctx._check(ctx.lib.fri_commit_device(ctx.h, dptr, dL, L, fri_amd.GENERATOR, None, 0, None,
-                                                 ctypes.byref(res)))
+            ctx._check(ctx.lib.fri_commit_device(ctx.h, dptr, dL, L, fri_amd.GENERATOR, None,
+                                                 fri_amd.FLAG_RANK_INPUTS, None, ctypes.byref(res)))
 
         if name.endswith("_primary"):
             out.update(step=step, res0=first, res=res, d=dL, coeffs=cf, verified=exp is not None, log_n=L)

@@ -77,6 +77,13 @@ typedef struct fri_ctx fri_ctx;
 #define FRI_FLAG_FORCE_BETAS 1u   /* test hook: use forced_betas[k] instead of the
                                      channel's draw (transcript still absorbs roots) */
 #define FRI_FLAG_NO_GRAPH    2u   /* run eagerly instead of replaying a hipGraph   */
+#define FRI_FLAG_RANK_INPUTS 4u   /* multi-GPU context, fri_commit_device with
+                                     fri_ctx_input_buffer(): every rank's own input
+                                     buffer already holds these coefficients (it
+                                     does after any team commit of them, until the
+                                     caller rewrites rank 0's buffer), so no rank
+                                     copies rank 0's over xGMI; FRI_ESTATE when a
+                                     rank has no input buffer of this shape yet */
 
 /* ---------------------------------------------------------------- context */
 /* Opens `device` (HIP ordinal) and sizes scratch for codewords up to

@@ -2991,10 +2991,25 @@ static int team_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t
     if (!out) return fail(ctx, FRI_EINVAL, "null argument");
     if (!team_shards(T, log_n))
         return run_commit(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
+    // FRI_FLAG_RANK_INPUTS: each rank reads its own input buffer (resident
+    // since the last team commit that staged these coefficients)
+    std::vector<const uint32_t*> din(T->G, dev_coeffs);
+    if (flags & FRI_FLAG_RANK_INPUTS) {
+        uint32_t logG = T->logG;
+        for (uint32_t r = 0; r < T->G; r++) {
+            const fri_ctx* c = T->rk[r];
+            const Plan& p = c->cur_lane == 0 ? c->plan : c->lanes[0].plan;
+            if (!p.valid || !p.sharded || p.d != d || p.log_n != log_n || p.offset != offset || p.G != T->G ||
+                (r == 0 && dev_coeffs != p.d_in) || log_n < logG)
+                return fail(ctx, FRI_ESTATE, "FRI_FLAG_RANK_INPUTS: commit these coefficients once without it, "
+                                             "and pass fri_ctx_input_buffer()");
+            din[r] = p.d_in;
+        }
+    }
+    const uint32_t fl = flags & ~FRI_FLAG_RANK_INPUTS;
     std::vector<fri_commit_result> res(T->G);
     int rc = team_run(ctx, [&](uint32_t r) {
-        return run_commit_sharded(T->rk[r], host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas,
-                                  &res[r]);
+        return run_commit_sharded(T->rk[r], host_coeffs, din[r], d, log_n, offset, chan_in, fl, forced_betas, &res[r]);
     });
     if (rc) return rc;
     // the redundant tops give every rank the whole transcript: they must agree

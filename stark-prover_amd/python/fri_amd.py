@@ -37,6 +37,7 @@ HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "fri_a
 FRI_OK, FRI_EINVAL, FRI_ENOMEM, FRI_EHIP, FRI_ENODEV, FRI_ERCCL, FRI_ESTATE, FRI_EDEGREE = range(8)
 FLAG_FORCE_BETAS = 1
 FLAG_NO_GRAPH = 2
+FLAG_RANK_INPUTS = 4      # FRI_FLAG_RANK_INPUTS (fri_amd.h): team commit from the ranks' resident inputs
 MAX_INFLIGHT = 4          # FRI_MAX_INFLIGHT (fri_amd.h): pipelined commits pending per context
 DEFAULT_LANES = 3         # FRI_DEFAULT_LANES (fri_amd.h): commit lanes of a context
 

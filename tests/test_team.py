@@ -190,6 +190,16 @@ def test_team_commit_device_from_rank0_buffer(team4, oracle, oracle_commit):
         team4._check(team4.lib.fri_commit_device(team4.h, p, cf.size, L, fri_amd.GENERATOR, None, 0, None,
                                                  ctypes.byref(out)))
         assert _transcript(out) == oracle_commit(L, 42)
+    # FRI_FLAG_RANK_INPUTS: every rank reads its own resident copy
+    for _ in range(2):
+        team4._check(team4.lib.fri_commit_device(team4.h, p, cf.size, L, fri_amd.GENERATOR, None,
+                                                 fri_amd.FLAG_RANK_INPUTS, None, ctypes.byref(out)))
+        assert _transcript(out) == oracle_commit(L, 42)
+    # ... which a rank without an input buffer of this shape cannot do
+    for bad in ((p, cf.size // 2), (ctypes.c_void_p(p.value + 64), cf.size)):
+        rc = team4.lib.fri_commit_device(team4.h, bad[0], bad[1], L, fri_amd.GENERATOR, None,
+                                         fri_amd.FLAG_RANK_INPUTS, None, ctypes.byref(out))
+        assert rc == fri_amd.FRI_ESTATE
 
 
 def test_team_create_arguments():
