@@ -122,6 +122,9 @@ __device__ __forceinline__ void pair_level(const uint4* A, uint4* B, uint32_t* o
 #ifndef FRI_SCHED_PRODUCER
 #define FRI_SCHED_PRODUCER 1
 #endif
+#ifndef FRI_SCHED_CHANNEL
+#define FRI_SCHED_CHANNEL FRI_SCHED_PRODUCER   // the channel's root blocks too (chan_produce)
+#endif
 struct SchedLds {
     uint32_t wk[32 * 48];       // per node W16..W63 + K (16-byte aligned rows of 48 words)
     uint32_t flag;
@@ -553,8 +556,12 @@ enum { CJ_REHASH = 0, CJ_MID = 2, CJ_ROOT = 3, CJ_FINAL = 6, CJ_END_ROUND = 6, C
 
 // Lane-pair form (sha256_quad.hpp): X is this lane's half of the chaining
 // value (even lane words 4..7, odd lane 0..3); cs stays whole on every lane.
+// wk (FRI_SCHED_PRODUCER): the two root-message blocks (jobs 3, 4) take their
+// rounds 16..63 from rows 0 / 1 of wk, made by chan_produce on wave 6; flags
+// base + 1 .. base + 6.
 __device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[4], uint32_t has, const uint4* root_lds,
-                                         uint32_t fv, const shaq::Role& R) {
+                                         uint32_t fv, const shaq::Role& R, const uint32_t* wk = nullptr,
+                                         const uint32_t* flag = nullptr, uint32_t base = 0) {
     uint32_t w[16];
     const bool pad = (j == 1) || (j == 5);
     if (j == 0 || j == 2 || j == 6) {
@@ -584,6 +591,7 @@ __device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[4], u
         w[15] = 80u * 8u;                           // hex(state) (64) + 16 chars
     }
     if (pad) shaq::compress_kw(X, j == 1 ? shaf::PAD_KW_C.kw : (has ? shaf::PAD_KW_1536.kw : shaf::PAD_KW_1024.kw), R);
+    else if (wk && (j == 3 || j == 4)) shaq::compress_ext(X, w, R, wk + 48 * (j - 3), flag, base + 3 * (j - 3));
     else shaq::compress(X, w, R);
     if (j == 1 || j == 5 || j == 7) {            // cs = X, both halves on every lane
 #pragma unroll
@@ -592,6 +600,24 @@ __device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[4], u
             cs[i] = R.is_a ? X[i] : o;
             cs[4 + i] = R.is_a ? o : X[i];
         }
+    }
+}
+
+// The schedules of the root message's two blocks (jobs 3 and 4: hex(hex(root))
+// in two 64-byte halves), on a producer wave while the channel wave runs the
+// rounds: both messages are known once the root is, so the producer makes
+// both rows (0, 1) in the iteration of job 3; flags base + 1 .. base + 6.
+__device__ __forceinline__ void chan_produce(const uint4* root_lds, SchedLds* sl, uint32_t base, const shaq::Role& R) {
+    const uint32_t lane = __lane_id();
+#pragma unroll 1
+    for (uint32_t jb = 0; jb < 2; jb++) {
+        const uint32_t b = (lane & 15u) + 16u * jb;
+        const uint32_t rw = reinterpret_cast<const uint32_t*>(root_lds)[b >> 2];
+        const uint32_t hh = hexhex((rw >> (24 - 8 * (b & 3))) & 255u);
+        uint32_t w[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) w[jj] = __builtin_amdgcn_readlane(hh, jj);
+        shaq::produce(w, sl->wk + 48 * jb, &sl->flag, base + 3 * jb, lane == 0, lane == 0, R);
     }
 }
 
@@ -748,11 +774,14 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     // iterations: the levels, then the channel jobs still left after them
     const uint32_t nlev = L - l;
     uint32_t total = nlev;
+    uint32_t it_root = ~0u;                        // the iteration of job 3 (the root's first block)
     if (COMMIT) {
         const uint32_t n_pre = !st->chan_has ? 0u : (st->chan_pending ? 3u : 1u);
         const uint32_t pre_in_levels = min(n_pre, min(nlev, 8u));   // levels with <= 128 nodes
         total += (n_pre - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
+        it_root = nlev + (n_pre - pre_in_levels);
     }
+    const bool chan_prod = FRI_SCHED_CHANNEL && COMMIT && tid >= 384 && tid < 448;   // wave 6 (SIMD 2)
     const shaq::Role R = shaq::role_of(tid);
     uint32_t cnt = N;
 #pragma unroll 1
@@ -790,9 +819,10 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         // channel job: during the narrow levels (SIMD 3 idle) only the
         // pre-root jobs, after the last level anything left
         if (chan_wave && job < job_end && (level ? (cnt <= 192 && job < CJ_ROOT) : true)) {
-            chan_job(job, cs, X, has, A, fv, R);
+            chan_job(job, cs, X, has, A, fv, R, FRI_SCHED_CHANNEL ? sl.wk : nullptr, &sl.flag, 3u * it_root);
             job++;
         }
+        if (chan_prod && it == it_root) chan_produce(A, &sl, 3u * it_root, R);
         lds_barrier();
         if (level) {
             uint4* tmp = A; A = B; B = tmp;
@@ -979,6 +1009,8 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
         const uint32_t npre_u = (li == 0) ? (!st->chan_has ? 0u : (st->chan_pending ? 3u : 1u)) : 3u;
         const uint32_t pre_in_levels = min(npre_u, min(nlev, 8u));
         const uint32_t total = nlev + (npre_u - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
+        const uint32_t it_root = nlev + (npre_u - pre_in_levels);   // iteration of job 3
+        uint32_t ch_base = 0;                                         // flag base of this layer's root blocks
         uint32_t cnt = N;
 #pragma unroll 1
         for (uint32_t it = 0; it < total; it++) {
@@ -1000,10 +1032,12 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
                     }
                 }
             }
+            if (!level && it == it_root) ch_base = 3u * (ord++), ord++;   // two ordinals (uniform)
             if (chan_wave && job < job_end && (level ? (cnt <= 192 && job < CJ_ROOT) : true)) {
-                chan_job(job, cs, X, has, A, fv, R);
+                chan_job(job, cs, X, has, A, fv, R, FRI_SCHED_CHANNEL ? sl.wk : nullptr, &sl.flag, ch_base);
                 job++;
             }
+            if (FRI_SCHED_CHANNEL && tid >= 384 && tid < 448 && !level && it == it_root) chan_produce(A, &sl, ch_base, R);
             lds_barrier();
             if (level) { uint4* tmp = A; A = B; B = tmp; }
         }

@@ -149,6 +149,26 @@ __device__ __forceinline__ void produce(uint32_t w[16], uint32_t* wk, uint32_t* 
     }
 }
 
+// Round wave: one block on a register message w[0..15] (rounds 0..15) whose
+// rounds 16..63 are fed from wk (W + K, written by produce); st += result.
+__device__ __forceinline__ void compress_ext(uint32_t st[4], const uint32_t w[16], const Role& R, const uint32_t* wk,
+                                             const uint32_t* flag, uint32_t base) {
+    uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+#pragma unroll
+    for (int i = 0; i < 16; i++) SHAQ_R(w[i] + shaf::KTAB[i]);
+#pragma unroll 1
+    for (int b = 0; b < 3; b++) {
+        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < base + b + 1) {}
+        const uint4* q = reinterpret_cast<const uint4*>(wk + 16 * b);
+        const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        SHAQ_R(q0.x); SHAQ_R(q0.y); SHAQ_R(q0.z); SHAQ_R(q0.w);
+        SHAQ_R(q1.x); SHAQ_R(q1.y); SHAQ_R(q1.z); SHAQ_R(q1.w);
+        SHAQ_R(q2.x); SHAQ_R(q2.y); SHAQ_R(q2.z); SHAQ_R(q2.w);
+        SHAQ_R(q3.x); SHAQ_R(q3.y); SHAQ_R(q3.z); SHAQ_R(q3.w);
+    }
+    st[0] += x0; st[1] += x1; st[2] += x2; st[3] += x3;
+}
+
 // Round wave: node SHA256(l || r) with the first block's rounds 16..63 fed
 // from wk (W + K, written by produce), then the padding block.  Same digest
 // halves as node().
