@@ -122,8 +122,11 @@ __device__ __forceinline__ void pair_level(const uint4* A, uint4* B, uint32_t* o
 #ifndef FRI_SCHED_PRODUCER
 #define FRI_SCHED_PRODUCER 1
 #endif
+// The channel's root blocks (jobs 3, 4) with their schedule on wave 6
+// (chan_produce): within noise, 4.612 vs 4.616 ms per 2^24 commit over 4
+// interleaved A/B rounds (profiles/r05_sched_channel_ab.txt), so off.
 #ifndef FRI_SCHED_CHANNEL
-#define FRI_SCHED_CHANNEL FRI_SCHED_PRODUCER   // the channel's root blocks too (chan_produce)
+#define FRI_SCHED_CHANNEL 0
 #endif
 struct SchedLds {
     uint32_t wk[32 * 48];       // per node W16..W63 + K (16-byte aligned rows of 48 words)
