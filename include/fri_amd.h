@@ -343,6 +343,11 @@ int fri_ctx_create_multi(const int* devices, uint32_t n_devices, uint32_t log_n_
  * its fri_debug_transport_log; owned by the team, never destroyed by the
  * caller (FRI_EINVAL). */
 int fri_debug_team_rank(fri_ctx* ctx, uint32_t rank, fri_ctx** out);
+/* Test hook (peer transport): the next team call makes rank `rank` fail
+ * with FRI_ERCCL at its op_index-th collective (0-based), as a rank whose
+ * transfer broke would; the other ranks must return instead of waiting for
+ * it.  Fires once; op_index < 0 clears it. */
+int fri_debug_team_inject_failure(fri_ctx* ctx, uint32_t rank, int64_t op_index);
 
 /* -------------------------------------------------------------- multi-GPU */
 /* One process per GPU.  A codeword of 2^log_n is committed by G ranks

@@ -95,6 +95,8 @@ struct Transport {
     bool loop = false;          // fri_debug_attach_loopback: every exchange returns this rank's own bytes
     bool peer = false;          // in-process team, peer transport (peer_op)
     Team* team = nullptr;       // the team this rank belongs to (peer or team RCCL transport)
+    int64_t fail_at = -1;       // fri_debug_team_inject_failure: peer op index (this call) that fails
+    int64_t n_ops = 0;          // peer ops issued by the current team call
     fri_collectives ops{};
     uint8_t* hs = nullptr;      // pinned staging
     uint8_t* hr = nullptr;
@@ -1925,6 +1927,10 @@ static int peer_op(fri_ctx* ctx, uint32_t op, uint32_t chan, const void* send, v
     Team* T = ctx->tp.team;
     const uint32_t r = (uint32_t)ctx->tp.rank, G = T->G;
     if (bytes % 4) return fail(ctx, FRI_EINVAL, "peer transport: byte count not a multiple of 4");
+    if (ctx->tp.fail_at >= 0 && ctx->tp.n_ops++ == ctx->tp.fail_at) {      // test hook: this rank fails here
+        ctx->tp.fail_at = -1;
+        return fail(ctx, FRI_ERCCL, std::string("injected failure at peer op ") + op_name(op));
+    }
     FRI_HIP(ctx, hipEventRecord(T->ev_ready[r], s));
     T->slot[r] = PeerSlot{send, recv, bytes, op, chan, peer};
     if (!team_barrier(T)) return fail(ctx, FRI_ERCCL, "peer transport: another rank failed (" + T->why + ")");
@@ -2797,6 +2803,7 @@ static int team_run(fri_ctx* root, const std::function<int(uint32_t)>& fn) {
         T->arrived = 0;
         T->why.clear();
     }
+    for (fri_ctx* c : T->rk) c->tp.n_ops = 0;     // (fri_debug_team_inject_failure counts per call)
     {
         std::lock_guard<std::mutex> g(T->jm);
         T->job = fn;
@@ -2941,6 +2948,15 @@ extern "C" int fri_ctx_create_multi(const int* devices, uint32_t n, uint32_t log
     T->rk[0]->team_root = T;
     (void)hipSetDevice(dev[0]);
     *out = T->rk[0];
+    return FRI_OK;
+}
+
+extern "C" int fri_debug_team_inject_failure(fri_ctx* ctx, uint32_t rank, int64_t op_index) {
+    if (!ctx) return FRI_EINVAL;
+    if (!ctx->team_root || ctx->team_root->kind != FRI_TRANSPORT_PEER)
+        return fail(ctx, FRI_EINVAL, "not a multi-GPU context on the peer transport");
+    if (rank >= ctx->team_root->G) return fail(ctx, FRI_EINVAL, "rank out of range");
+    ctx->team_root->rk[rank]->tp.fail_at = op_index;
     return FRI_OK;
 }
 

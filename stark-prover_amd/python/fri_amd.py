@@ -98,6 +98,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_ctx_create": (i32, [i32, u32, ctypes.POINTER(vp)]),
         "fri_ctx_create_multi": (i32, [ctypes.POINTER(i32), u32, u32, i32, ctypes.POINTER(vp)]),
         "fri_debug_team_rank": (i32, [vp, u32, ctypes.POINTER(vp)]),
+        "fri_debug_team_inject_failure": (i32, [vp, u32, ctypes.c_int64]),
         "fri_ctx_destroy": (i32, [vp]),
         "fri_last_error": (ctypes.c_char_p, [vp]),
         "fri_version": (ctypes.c_char_p, []),
@@ -226,6 +227,11 @@ class Context:
         h = ctypes.c_void_p()
         self._check(self.lib.fri_debug_team_rank(self.h, rank, ctypes.byref(h)))
         return Context(self.device, self.log_n_max, _handle=h, _owner=False)
+
+    def inject_team_failure(self, rank: int, op_index: int):
+        """Test hook (fri_debug_team_inject_failure): rank `rank` fails its
+        op_index-th collective in the next team call."""
+        self._check(self.lib.fri_debug_team_inject_failure(self.h, rank, op_index))
 
     def close(self):
         if self.h and self._owner:

@@ -176,6 +176,27 @@ def test_team_errors_then_recovers(team4, oracle, oracle_commit):
     assert e.value.code == fri_amd.FRI_EINVAL
 
 
+@pytest.mark.parametrize("rank,op", [(2, 0), (1, 3), (3, 7), (0, 5)])   # 8 collectives at 2^22 x 4
+def test_team_rank_failure_does_not_block(team4, oracle, oracle_commit, rank, op):
+    """One rank fails at its op-th collective (fri_debug_team_inject_failure,
+    as a broken transfer would): the call returns FRI_ERCCL naming that rank
+    and op instead of leaving the other ranks waiting at the rendezvous, every
+    rank's streams are drained, and the next team commit is right."""
+    import time
+
+    import fri_amd
+    L = 22
+    cf = _coeffs(oracle, 17, L)
+    team4.inject_team_failure(rank, op)
+    t0 = time.time()
+    with pytest.raises(fri_amd.FriError) as e:
+        team4.commit(cf, L)
+    assert e.value.code == fri_amd.FRI_ERCCL
+    assert f"rank {rank}" in str(e.value) and "injected failure" in str(e.value), str(e.value)
+    assert time.time() - t0 < 30
+    assert _transcript(team4.commit(cf, L)) == oracle_commit(L, 17)
+
+
 def test_team_commit_device_from_rank0_buffer(team4, oracle, oracle_commit):
     """fri_commit_device on the team: the context's input buffer (rank 0's
     device) is read by rank 0 in place and copied by the other ranks."""
