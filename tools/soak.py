@@ -49,7 +49,8 @@ def transcript(r):
 class Driven:
     """One context and the model of its state: the result slot of every
     pending ticket (lowest free slot, fri_api.hip async_enqueue), its lanes,
-    its shape and what its input buffer holds in call order."""
+    its shape and what its input buffer holds in call order (a pipelined
+    commit dealt to lane 0 stages its coefficients there)."""
 
     def __init__(self, fri_amd, polys, rng):
         self.fa, self.polys, self.rng = fri_amd, polys, rng
@@ -60,9 +61,6 @@ class Driven:
         self.L = SHAPES[0]
         self.in_buf = None
         self.n_ok = 0
-
-    def next_lane(self):
-        return min(set(range(self.fa.MAX_INFLIGHT)) - set(self.slots.values())) % self.lanes
 
     def enqueue(self, t, key):
         self.slots[t] = min(set(range(self.fa.MAX_INFLIGHT)) - set(self.slots.values()))
@@ -111,11 +109,13 @@ class Driven:
             self.n_ok += 1
             self.in_buf = (L, j)
         elif kind in (2, 3):                       # pipelined, device buffer / host coefficients
-            lane0 = self.next_lane() == 0
             t = ctx.commit_device_async(dev.data_ptr(), d, L) if kind == 2 else ctx.commit_async(c, L)
             self.enqueue(t, (L, j))
-            if lane0:
-                self.in_buf = (L, j)               # a lane-0 commit stages its input into the input buffer
+            # a commit dealt to lane 0 stages its input into the input buffer
+            # (the deal itself, fewest pending first, is the library's:
+            # fri_debug_ticket_lane reports it)
+            if ctx.ticket_lane(t) == 0:
+                self.in_buf = (L, j)
         else:                                      # pipelined, the context's own input buffer
             p0 = ctypes.c_void_p()
             ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(p0)))
