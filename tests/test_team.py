@@ -264,3 +264,54 @@ def test_team_2p28_world8_configs4(oracle_commit):
             assert h.hex() == want["roots"][k], k
     finally:
         cx.close()
+
+
+_TF = int(os.environ.get("TEAM_FUZZ_N", "0"))      # > 0: that many cases per team size (longer runs)
+
+
+@pytest.mark.parametrize("G,n_cases", [(2, _TF or 8), (4, _TF or 8), (8, _TF or 6)])
+def test_team_fuzz_vs_c_oracle(G, n_cases, corc, oracle):
+    """Randomised team commits (the sharded fuzz's cases, dist_worker.fuzz_case:
+    2^20..2^22, ragged coefficient counts including 0, blowups 1..16, degrees
+    that end inside the sharded layers, zero / constant / odd-only polynomials,
+    random cosets, prefilled channels, forced betas on every third case) on a
+    team of G ranks on GPU 0 (peer transport), one fri_commit call each:
+    the whole transcript equals the OpenMP C oracle's 1-node commit
+    (orc_fri_commit_fast, src/fri/fri_commit.rs:72-122), and the ranks'
+    transport logs pass the cross-rank schedule check."""
+    import fri_amd
+    from dist_worker import fuzz_case, fuzz_forced_betas
+    from test_dist import check_transport_schedule
+    seed = 1000 * G + 7
+    cx = fri_amd.Context.multi([0] * G, 22, transport="peer")
+    try:
+        for i in range(n_cases):
+            log_n, c, offset, state = fuzz_case(seed + i, G)
+            fb = fuzz_forced_betas(seed + i)
+            res = cx.commit(np.asarray(c, dtype=np.uint32), log_n, offset=offset, channel_state=state,
+                            forced_betas=fb)
+            fbp = None
+            if fb is not None:
+                fba = np.ascontiguousarray(np.array(fb, dtype=np.uint64))
+                fbp = fba.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+            cs = np.ascontiguousarray(c, dtype=np.uint64)
+            och = oracle.OrcChannel()
+            corc.orc_channel_init(ctypes.byref(och))
+            if state is not None:
+                och.state = state.hex().encode()
+                och.state_len = 64
+            ores = oracle.OrcFriResult()
+            assert corc.orc_fri_commit_fast(cs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), c.size, log_n,
+                                            offset, 5, oracle.P, ctypes.byref(och), fbp, ctypes.byref(ores), None,
+                                            None) == 0
+            what = (f"case {seed + i}: G={G} log_n={log_n} d={c.size} offset={offset} "
+                    f"prefilled={state is not None} forced={fb is not None}")
+            want = {"roots": [bytes(ores.roots[k]).hex() for k in range(ores.n_layers)],
+                    "betas": [int(ores.betas[j]) for j in range(ores.n_rounds)],
+                    "final_value": int(ores.final_value), "final_degree": int(ores.final_degree),
+                    "state": och.state.decode()}
+            assert _transcript(res) == want, what
+            if log_n >= 20:
+                check_transport_schedule([cx.team_rank(r).transport_log() for r in range(G)])
+    finally:
+        cx.close()
