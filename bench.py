@@ -566,6 +566,29 @@ def main():
             roofline["traffic"] = traffic
             roofline["traffic_note"] = traffic_note
 
+    # A second multi-GPU point from the same job: after the RCCL run, rank 0
+    # drives every GPU of the job as one team context (peer transport over
+    # xGMI) on the primary codeword while the other ranks wait.  Beside
+    # `value`, never it.
+    if mode == "sharded" and not team_n and world > 1 and not args.no_secondary and pg is not None:
+        barrier_sync()
+        if rank == 0:
+            try:
+                ts = _team_stage(fri_amd, [r % max(ndev_all, 1) for r in range(world)],
+                                 [("strong_primary", log_n)], args, _plain_timed)
+                k = max(3, args.steps // 4)
+                el = _plain_timed(ts["step"], k, 1)
+                secondary["p2p_team"] = {"codeword_log2": log_n, "ranks": world, "ms_per_step": round(1000 * el / k, 4),
+                                         "value": round((1 << log_n) * k / el, 1), "unit": "field-elems/s",
+                                         "steps": k, "oracle_verified": bool(ts["verified"]),
+                                         "transport": ts["dist_report"],
+                                         "what": "the same codeword from ONE process: fri_ctx_create_multi over "
+                                                 "the job's GPUs, one fri_commit_device call per step"}
+                ts["ctx"].close()
+            except Exception as e:  # noqa: BLE001 - reported beside the line
+                secondary["p2p_team"] = {"error": f"{type(e).__name__}: {e}"}
+        barrier_sync()
+
     b_field, b_tree = algorithmic_bytes(log_n, d)
     whole = {"B_alg_bytes": b_field + b_tree, "B_field_bytes": b_field, "B_tree_bytes": b_tree,
              "achieved_GBs": round((b_field + b_tree) / (ms_per_step * 1e-3) / 1e9, 2),
