@@ -47,6 +47,28 @@ constexpr uint32_t INV2_M2 = 0x80000000u;   // Montgomery(2^-1) = 2^31 mod p
 #define TOP_CLK(i) do {} while (0)
 #define TOP_STAMP_T(i, tid_) do {} while (0)
 #endif
+// workgroup 0 of a wide leaf kernel: start, leaves done, levels done (60..62)
+#ifdef FRI_STAMPS
+#define WIDE_STAMP(i)                                                                              \
+    do {                                                                                           \
+        if (COMMIT && blockIdx.x == 0 && threadIdx.x == 0) t.st->stamps[t.k][(i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define WIDE_STAMP(i) do {} while (0)
+#endif
+// the same marks for a layer of the tail kernel (t: that layer's task)
+#ifdef FRI_STAMPS
+#define TAIL_STAMP_T(i, tid_, fn)                                                  \
+    do {                                                                           \
+        if (threadIdx.x == (tid_)) t.st->stamps[t.k][(i)] = fn();                  \
+    } while (0)
+#define TAIL_STAMP(i) TAIL_STAMP_T(i, 0, __builtin_amdgcn_s_memrealtime)
+#define TAIL_CLK(i) TAIL_STAMP_T(i, 0, __builtin_amdgcn_s_memtime)
+#else
+#define TAIL_STAMP_T(i, tid_, fn) do {} while (0)
+#define TAIL_STAMP(i) do {} while (0)
+#define TAIL_CLK(i) do {} while (0)
+#endif
 
 __device__ __forceinline__ uint32_t fold1(uint32_t a, uint32_t b, uint32_t xinv_m, uint32_t beta_m) {
     uint32_t s = add(a, b), t = sub(a, b);
@@ -180,8 +202,13 @@ __device__ __forceinline__ int wave_max_i(int v) {
 // Coefficient task of one workgroup (w of G): k == 0 -> max nonzero index
 // of the input (deg_0); k >= 1 -> fold slice c'_j = c_2j + beta c_2j+1 with
 // maxima of c', even part, odd part.  Results: wgmax[3w .. 3w+2].
-__device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red /*LDS [3*waves]*/) {
+// coef_slice: the slice over threads [t0, t0 + nthr) (whole waves), per-wave
+// maxima into red[3 * (wave - t0 / 64) ..]; coef_combine (one thread, after a
+// barrier): red -> wgmax.
+__device__ __forceinline__ void coef_slice(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red, uint32_t t0,
+                                           uint32_t nthr) {
     int m0 = -1, m1 = -1, m2 = -1;
+    const uint32_t tx = threadIdx.x - t0;
     // this rank's coefficient range (all of poly_k unless sharded), split
     // evenly over the G workgroups; indices j are global
     const size_t jhi_all = t.jhi ? t.jhi : ~(size_t)0;
@@ -191,7 +218,7 @@ __device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32
         const size_t a = t.jlo, b = min(t.d0, jhi_all), n = b > a ? b - a : 0;
         const size_t cs = (n + G - 1) / G, lo = a + (size_t)w * cs, hi = min(b, lo + cs);
         const uint32_t* in = t.coef_in - t.ibase;
-        for (size_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+        for (size_t j = lo + tx; j < hi; j += nthr) {
             const uint32_t c = in[j];
             if (c) m0 = max(m0, (int)j);
             if (c >= P) m1 = 0;
@@ -204,7 +231,7 @@ __device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32
         const size_t cs = (n + G - 1) / G, lo = a + (size_t)w * cs, hi = min(b, lo + cs);
         const uint32_t* in = t.coef_in - t.ibase;
         uint32_t* outp = t.coef_out - t.obase;
-        for (size_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+        for (size_t j = lo + tx; j < hi; j += nthr) {
             uint32_t e = in[2 * j];
             uint32_t o = (2 * j + 1 < len) ? in[2 * j + 1] : 0u;
             uint32_t v = add(e, mmul(o, beta_m));
@@ -215,14 +242,18 @@ __device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32
         }
     }
     m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
-    const uint32_t wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[3 * wave] = m0; red[3 * wave + 1] = m1; red[3 * wave + 2] = m2; }
+    const uint32_t wave = tx >> 6;
+    if ((tx & 63) == 0) { red[3 * wave] = m0; red[3 * wave + 1] = m1; red[3 * wave + 2] = m2; }
+}
+__device__ __forceinline__ void coef_combine(const LayerTask& t, uint32_t w, const int32_t* red, uint32_t nw) {
+    int a = -1, b = -1, c = -1;
+    for (uint32_t i = 0; i < nw; i++) { a = max(a, red[3 * i]); b = max(b, red[3 * i + 1]); c = max(c, red[3 * i + 2]); }
+    t.wgmax[3 * w] = a; t.wgmax[3 * w + 1] = b; t.wgmax[3 * w + 2] = c;
+}
+__device__ __forceinline__ void coef_task(const LayerTask& t, uint32_t w, uint32_t G, int32_t* red /*LDS [3*waves]*/) {
+    coef_slice(t, w, G, red, 0, blockDim.x);
     lds_barrier();          // red[] only: the leaf digest stores need not drain here
-    if (threadIdx.x == 0) {
-        int a = -1, b = -1, c = -1;
-        for (uint32_t i = 0; i < blockDim.x / 64; i++) { a = max(a, red[3 * i]); b = max(b, red[3 * i + 1]); c = max(c, red[3 * i + 2]); }
-        t.wgmax[3 * w] = a; t.wgmax[3 * w + 1] = b; t.wgmax[3 * w + 2] = c;
-    }
+    if (threadIdx.x == 0) coef_combine(t, w, red, blockDim.x / 64);
 }
 
 #ifndef FRI_QUAD_LEAVES_FIRST
@@ -343,6 +374,7 @@ __host__ __device__ __forceinline__ uint32_t wide_levels(uint32_t L) { return L 
 template <bool FOLD, bool COMMIT, bool PAIR = false>
 __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
     if (gated_off(t)) return;
+    WIDE_STAMP(60);
     __shared__ uint4 lds[2 * 256 + 2 * 128];
     __shared__ int32_t red[12];
     __shared__ SchedLds sl;
@@ -367,8 +399,8 @@ __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
     uint4* A = lds;
     uint4* B = lds + 2 * 256;
     dg_lds_store(A + 2 * threadIdx.x, d);
-    if (COMMIT) coef_task(t, blockIdx.x, gridDim.x, red);
     lds_barrier();
+    WIDE_STAMP(61);
     uint32_t cnt = 256;
     const shaq::Role qr = shaq::role_of(threadIdx.x);
     if (grid * 128 < WIDE_PAIR_MAX) chain_prio();   // from level 1 on, all on lane pairs
@@ -387,9 +419,14 @@ __global__ __launch_bounds__(256) void k_layer_leaf_wide(LayerTask t) {
             dg_lds_store(B + 2 * threadIdx.x, o);
             dg_store(out + 8 * threadIdx.x, o);
         }
+        // the coefficient slice (needed only by the layer's top kernel) on
+        // waves 2-3, idle from level 2 on: off the tree's critical path
+        if (COMMIT && j == 2 && threadIdx.x >= 128) coef_slice(t, blockIdx.x, gridDim.x, red, 128, 128);
         lds_barrier();
         uint4* tmp = A; A = B; B = tmp;
     }
+    if (COMMIT && threadIdx.x == 128) coef_combine(t, blockIdx.x, red, 2);   // nlev >= 4: red[] settled
+    WIDE_STAMP(62);
 }
 
 // Reduce the coefficient-maxima triples of the R producer workgroups of this
@@ -822,7 +859,17 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         // channel job: during the narrow levels (SIMD 3 idle) only the
         // pre-root jobs, after the last level anything left
         if (chan_wave && job < job_end && (level ? (cnt <= 192 && job < CJ_ROOT) : true)) {
+#ifdef FRI_STAMPS
+            if (job == CJ_ROOT) TOP_STAMP_T(14, 448);               // job 3 / job 5 start (14, 13)
+            if (job == CJ_ROOT + 2) TOP_STAMP_T(13, 448);
+#endif
             chan_job(job, cs, X, has, A, fv, R, FRI_SCHED_CHANNEL ? sl.wk : nullptr, &sl.flag, 3u * it_root);
+#ifdef FRI_STAMPS
+            if (job >= CJ_ROOT && job <= CJ_ROOT + 2) {          // the post-root jobs, done (20..22)
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                TOP_STAMP_T(20 + job - CJ_ROOT, 448);
+            }
+#endif
             job++;
         }
         if (chan_prod && it == it_root) chan_produce(A, &sl, 3u * it_root, R);
@@ -910,12 +957,24 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
     __shared__ uint32_t s_beta_m, s_active;
     __shared__ int32_t s_deg;
     __shared__ uint32_t s_fbeta[TAIL_LOG + 2];   // the test hook's betas of these layers (0: not forced)
+    __shared__ uint32_t xv[2 * NMAX];            // every layer's x^-1 table (prefetched)
     __shared__ SchedLds sl;
     sched_init(&sl);
     uint32_t ord = 0;                            // narrow levels so far (schedule producer flag)
     const uint32_t tid = threadIdx.x;
     const bool chan_wave = tid >= 448;
     DevState* st = t0.st;
+    // The x^-1 tables of layers 1.. are loaded into LDS by wave 6 during the
+    // first layer's levels (one HBM latency for the launch, off the chain,
+    // instead of one per layer fold); layer 0 folds from HBM.
+    auto prefetch_x = [&](uint32_t t0p, uint32_t nthr) {
+        uint32_t off = 1u << tt.t[0].L;
+        for (uint32_t li = 1; li < tt.n; li++) {
+            const uint32_t N = 1u << tt.t[li].L;
+            for (uint32_t j = tid - t0p; j < N; j += nthr) xv[off + j] = tt.t[li].xinv[j];
+            off += N;
+        }
+    };
     uint32_t cs[8], X[4];
     uint32_t has = 0;
     if (chan_wave) {
@@ -933,11 +992,14 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
     uint32_t beta_m = FOLD0 ? st->beta_mont[t0.k - 1] : 0u;
     int prev_deg = FOLD0 ? st->deg[t0.k - 1] : -1;
     const shaq::Role R = shaq::role_of(tid);
+    uint32_t xoff = 0;
 #pragma unroll 1
     for (uint32_t li = 0; li < tt.n; li++) {
         const LayerTask& t = tt.t[li];
         const int k = t.k;
         const uint32_t L = t.L, N = 1u << L;
+        const uint32_t* xl = li ? xv + xoff : t.xinv;
+        xoff += N;
         const bool fold = FOLD0 || li > 0;
         uint32_t* cur_v = vals[li & 1];
         const uint32_t* prev_v = vals[(li & 1) ^ 1];
@@ -946,6 +1008,7 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
         uint4* A = lds;
         uint4* B = lds + 2 * NMAX;
         uint32_t* tr = t.tree;
+        TAIL_STAMP(0);
         // ---- fold + leaves (spare lanes of wave 0 recompute leaf i mod N) ----
         for (uint32_t i = tid; i < max(N, 64u); i += blockDim.x) {
             const uint32_t j = i & (N - 1);
@@ -953,7 +1016,7 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
             uint32_t v;
             if (fold) {
                 const uint32_t a = li ? prev_v[j] : t.prev[j], b = li ? prev_v[j + N] : t.prev[j + N];
-                v = fold1(a, b, t.xinv[j], beta_m);
+                v = fold1(a, b, xl[j], beta_m);
                 if (real) t.values[j] = v;
             } else {
                 v = t.values[j];
@@ -967,51 +1030,66 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
             }
         }
         // ---- coefficient fold of round k-1 (or the input scan at k == 0) ----
-        int m0 = -1, m1 = -1, m2 = -1;
-        if (k == 0) {
-            for (size_t j = tid; j < t.d0; j += blockDim.x) {
-                const uint32_t c = t.coef_in[j];
-                if (c) m0 = max(m0, (int)j);
-                if (c >= P) m1 = 0;                    // not canonical (see coef_task)
+        // Needed only for the degree, i.e. from the root on: it runs on waves
+        // 4-5 (threads [256, 384)) during the first level iteration that
+        // leaves them idle (coef_it), unless the layer has no such level.
+        const uint32_t nlev = L;
+        const uint32_t coef_it = N > 256 ? 1u : 0u;   // iteration 0 of a 512-leaf layer uses all waves
+        const bool coef_late = nlev > coef_it;
+        auto coef_fold = [&](uint32_t t0c, uint32_t nthr) {
+            int m0 = -1, m1 = -1, m2 = -1;
+            const uint32_t tx = tid - t0c;
+            if (k == 0) {
+                for (size_t j = tx; j < t.d0; j += nthr) {
+                    const uint32_t c = t.coef_in[j];
+                    if (c) m0 = max(m0, (int)j);
+                    if (c >= P) m1 = 0;                    // not canonical (see coef_task)
+                }
+            } else {
+                const uint32_t len = (uint32_t)(prev_deg + 1), nlen = (len + 1) / 2;
+                const bool in_lds = li > 0 && k >= 2;      // poly_{k-1} was folded by this kernel
+                for (uint32_t j = tx; j < nlen; j += nthr) {
+                    const uint32_t e = in_lds ? prev_c[2 * j] : t.coef_in[2 * j];
+                    const uint32_t o = (2 * j + 1 < len) ? (in_lds ? prev_c[2 * j + 1] : t.coef_in[2 * j + 1]) : 0u;
+                    const uint32_t v = add(e, mmul(o, beta_m));
+                    cur_c[j] = v;
+                    if (v) m0 = (int)j;
+                    if (e) m1 = (int)j;
+                    if (o) m2 = (int)j;
+                }
             }
-        } else {
-            const uint32_t len = (uint32_t)(prev_deg + 1), nlen = (len + 1) / 2;
-            const bool in_lds = li > 0 && k >= 2;      // poly_{k-1} was folded by this kernel
-            for (uint32_t j = tid; j < nlen; j += blockDim.x) {
-                const uint32_t e = in_lds ? prev_c[2 * j] : t.coef_in[2 * j];
-                const uint32_t o = (2 * j + 1 < len) ? (in_lds ? prev_c[2 * j + 1] : t.coef_in[2 * j + 1]) : 0u;
-                const uint32_t v = add(e, mmul(o, beta_m));
-                cur_c[j] = v;
-                if (v) m0 = (int)j;
-                if (e) m1 = (int)j;
-                if (o) m2 = (int)j;
-            }
-        }
-        m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
-        if ((tid & 63) == 0) { red[3 * (tid >> 6)] = m0; red[3 * (tid >> 6) + 1] = m1; red[3 * (tid >> 6) + 2] = m2; }
+            m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
+            const uint32_t w = tx >> 6;
+            if ((tx & 63) == 0) { red[3 * w] = m0; red[3 * w + 1] = m1; red[3 * w + 2] = m2; }
+        };
+        if (!coef_late) coef_fold(0, blockDim.x);
+        if (li == 0 && !coef_late) prefetch_x(0, blockDim.x);
         lds_barrier();
-        int deg;
-        bool noncanon;
-        {
+        TAIL_STAMP(1);
+        TAIL_CLK(17);
+        int deg = 1;
+        bool noncanon = false;
+        int job_end = CJ_END_ROUND;                    // provisional while the degree is pending
+        uint32_t fv = 0;                               // fri_commit.rs:109-113
+        // red[] (after a barrier) -> degree of poly_k; is it the last layer?
+        auto settle = [&](uint32_t nw) {
             int a = -1, b = -1, c = -1;
-#pragma unroll
-            for (int i = 0; i < 8; i++) { a = max(a, red[3 * i]); b = max(b, red[3 * i + 1]); c = max(c, red[3 * i + 2]); }
+            for (uint32_t i = 0; i < nw; i++) { a = max(a, red[3 * i]); b = max(b, red[3 * i + 1]); c = max(c, red[3 * i + 2]); }
             deg = (k == 0) ? a : (b < 0 ? c : a);
             noncanon = k == 0 && b >= 0;
-        }
-        const bool is_final = deg < 1;
-        const int job_end = is_final ? CJ_END_FINAL : CJ_END_ROUND;
-        uint32_t fv = 0;                               // fri_commit.rs:109-113
-        if (chan_wave && is_final && deg == 0) fv = (k == 0) ? t.coef_in[0] : cur_c[0];
+            job_end = deg < 1 ? CJ_END_FINAL : CJ_END_ROUND;
+            if (chan_wave && deg == 0) fv = (k == 0) ? t.coef_in[0] : cur_c[0];
+        };
+        if (!coef_late) settle(8);
         // ---- levels + channel jobs (k_tree_top) ----
         int job = CJ_END_FINAL;
         if (chan_wave) job = !has ? CJ_ROOT : (pending ? CJ_REHASH : CJ_MID);
-        const uint32_t nlev = L;
         // uniform count of loop iterations: the channel prework count is the
-        // same on every lane (has / pending follow the layer index)
+        // same on every lane (has / pending follow the layer index); the
+        // channel jobs after the root follow the degree (settled by then)
         const uint32_t npre_u = (li == 0) ? (!st->chan_has ? 0u : (st->chan_pending ? 3u : 1u)) : 3u;
         const uint32_t pre_in_levels = min(npre_u, min(nlev, 8u));
-        const uint32_t total = nlev + (npre_u - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
+        uint32_t total = nlev + (npre_u - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
         const uint32_t it_root = nlev + (npre_u - pre_in_levels);   // iteration of job 3
         uint32_t ch_base = 0;                                         // flag base of this layer's root blocks
         uint32_t cnt = N;
@@ -1022,7 +1100,9 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
                 cnt >>= 1;
                 uint32_t* out = tr + 8 * level_offset(L, 1 + it);
                 if (cnt <= 128) {
+                    if (it < 18) TAIL_CLK(24 + 2 * it);
                     pair_level_s(A, B, out, tid, cnt, R, &sl, ord++);
+                    if (it < 18) TAIL_CLK(25 + 2 * it);
                 } else {
 #pragma unroll 1
                     for (uint32_t q = tid; q < cnt; q += blockDim.x) {
@@ -1038,11 +1118,24 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
             if (!level && it == it_root) ch_base = 3u * (ord++), ord++;   // two ordinals (uniform)
             if (chan_wave && job < job_end && (level ? (cnt <= 192 && job < CJ_ROOT) : true)) {
                 chan_job(job, cs, X, has, A, fv, R, FRI_SCHED_CHANNEL ? sl.wk : nullptr, &sl.flag, ch_base);
+#ifdef FRI_STAMPS
+                if (job >= CJ_ROOT && job <= CJ_ROOT + 2) TAIL_STAMP_T(20 + job - CJ_ROOT, 448, __builtin_amdgcn_s_memrealtime);
+#endif
                 job++;
             }
             if (FRI_SCHED_CHANNEL && tid >= 384 && tid < 448 && !level && it == it_root) chan_produce(A, &sl, ch_base, R);
+            if (coef_late && it == coef_it && tid >= 256 && tid < 384) coef_fold(256, 128);
+            if (li == 0 && coef_late && it == coef_it && tid >= 384 && tid < 448) prefetch_x(384, 64);
             lds_barrier();
-            if (level) { uint4* tmp = A; A = B; B = tmp; }
+            if (coef_late && it == coef_it) {
+                settle(2);
+                total = nlev + (npre_u - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
+            }
+            if (level) {
+                uint4* tmp = A; A = B; B = tmp;
+                if (it < 11) TAIL_STAMP(2 + it);
+                if (it + 1 == nlev) { TAIL_CLK(18); TAIL_STAMP(19); }
+            }
         }
         // ---- results (one lane of wave 7), hand-off to the next layer ----
         if (tid == 448 && noncanon) {                   // FRI_EINVAL (uniform: the loop ends below)
@@ -1086,6 +1179,7 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
             s_beta_m = bm;
             s_active = active;
             s_deg = deg;
+            TAIL_STAMP_T(15, 448, __builtin_amdgcn_s_memrealtime);
         }
         if (chan_wave) { has = 1; pending = 1; }
         lds_barrier();
