@@ -602,6 +602,11 @@ enum { CJ_REHASH = 0, CJ_MID = 2, CJ_ROOT = 3, CJ_FINAL = 6, CJ_END_ROUND = 6, C
 __device__ __forceinline__ void chan_job(int j, uint32_t cs[8], uint32_t X[4], uint32_t has, const uint4* root_lds,
                                          uint32_t fv, const shaq::Role& R, const uint32_t* wk = nullptr,
                                          const uint32_t* flag = nullptr, uint32_t base = 0) {
+    // the job and the channel flags are wave-uniform: in SGPRs the job's
+    // branches are scalar and its padding table is read by scalar loads
+    // (a per-lane table pointer costs a vector-load round trip per 16 rounds)
+    j = __builtin_amdgcn_readfirstlane(j);
+    has = __builtin_amdgcn_readfirstlane(has);
     uint32_t w[16];
     const bool pad = (j == 1) || (j == 5);
     if (j == 0 || j == 2 || j == 6) {

@@ -1,4 +1,5 @@
 set -e
 mkdir -p gpurun_out
-bash tools/pmc_icache.sh libfri_amd.so > gpurun_out/r05_pmc_icache.log 2>&1
-python3 tools/pmc_summary.py gpurun_out/pmc_ic_libfri_amd k_tree_top k_tree_tail k_tree_mid8 k_layer_leaf_wide > gpurun_out/r05_pmc_icache_summary.txt
+FRI_AMD_LIB=libfri_amd_stamps.so timeout -k 10 120 python3 -u stark-prover_amd/bench/stamps.py 24 > gpurun_out/r05t_stamps6.txt 2>&1
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -k "commit or tiny or merkle or trace" --timeout 300 --timeout-method thread > gpurun_out/r05t_uni_parity.log 2>&1
+bash tools/abn.sh 5 40 libfri_amd_prev.so libfri_amd.so 2>/dev/null > gpurun_out/r05_ab_uniform_job.txt
