@@ -816,16 +816,11 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         fv = SHARD ? t.shard->recs_in[11] : (t.k == 0 ? t.coef_in : t.coef_out)[0];
     TOP_STAMP(1);
     TOP_CLK(17);
-    // iterations: the levels, then the channel jobs still left after them
+    // iterations: the levels, then one in which wave 7 runs every channel
+    // job still left (no barrier between the post-root jobs)
     const uint32_t nlev = L - l;
-    uint32_t total = nlev;
-    uint32_t it_root = ~0u;                        // the iteration of job 3 (the root's first block)
-    if (COMMIT) {
-        const uint32_t n_pre = !st->chan_has ? 0u : (st->chan_pending ? 3u : 1u);
-        const uint32_t pre_in_levels = min(n_pre, min(nlev, 8u));   // levels with <= 128 nodes
-        total += (n_pre - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
-        it_root = nlev + (n_pre - pre_in_levels);
-    }
+    const uint32_t total = nlev + (COMMIT ? 1u : 0u);
+    const uint32_t it_root = COMMIT ? nlev : ~0u;  // the iteration of job 3 (the root's first block)
     const bool chan_prod = FRI_SCHED_CHANNEL && COMMIT && tid >= 384 && tid < 448;   // wave 6 (SIMD 2)
     const shaq::Role R = shaq::role_of(tid);
     uint32_t cnt = N;
@@ -864,18 +859,17 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         // channel job: during the narrow levels (SIMD 3 idle) only the
         // pre-root jobs, after the last level anything left
         if (chan_wave && job < job_end && (level ? (cnt <= 192 && job < CJ_ROOT) : true)) {
+            do {
 #ifdef FRI_STAMPS
-            if (job == CJ_ROOT) TOP_STAMP_T(14, 448);               // job 3 / job 5 start (14, 13)
-            if (job == CJ_ROOT + 2) TOP_STAMP_T(13, 448);
+                if (job == CJ_ROOT) TOP_STAMP_T(14, 448);           // job 3 / job 5 start (14, 13)
+                if (job == CJ_ROOT + 2) TOP_STAMP_T(13, 448);
 #endif
-            chan_job(job, cs, X, has, A, fv, R, FRI_SCHED_CHANNEL ? sl.wk : nullptr, &sl.flag, 3u * it_root);
+                chan_job(job, cs, X, has, A, fv, R, FRI_SCHED_CHANNEL ? sl.wk : nullptr, &sl.flag, 3u * it_root);
 #ifdef FRI_STAMPS
-            if (job >= CJ_ROOT && job <= CJ_ROOT + 2) {          // the post-root jobs, done (20..22)
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                TOP_STAMP_T(20 + job - CJ_ROOT, 448);
-            }
+                if (job >= CJ_ROOT && job <= CJ_ROOT + 2) TOP_STAMP_T(20 + job - CJ_ROOT, 448);   // done (20..22)
 #endif
-            job++;
+                job++;
+            } while (!level && job < job_end);
         }
         if (chan_prod && it == it_root) chan_produce(A, &sl, 3u * it_root, R);
         lds_barrier();
@@ -1089,13 +1083,10 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
         // ---- levels + channel jobs (k_tree_top) ----
         int job = CJ_END_FINAL;
         if (chan_wave) job = !has ? CJ_ROOT : (pending ? CJ_REHASH : CJ_MID);
-        // uniform count of loop iterations: the channel prework count is the
-        // same on every lane (has / pending follow the layer index); the
-        // channel jobs after the root follow the degree (settled by then)
-        const uint32_t npre_u = (li == 0) ? (!st->chan_has ? 0u : (st->chan_pending ? 3u : 1u)) : 3u;
-        const uint32_t pre_in_levels = min(npre_u, min(nlev, 8u));
-        uint32_t total = nlev + (npre_u - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
-        const uint32_t it_root = nlev + (npre_u - pre_in_levels);   // iteration of job 3
+        // the levels, then one iteration in which wave 7 runs every channel
+        // job still left (their number follows the degree, settled by then)
+        const uint32_t total = nlev + 1;
+        const uint32_t it_root = nlev;                                // iteration of job 3
         uint32_t ch_base = 0;                                         // flag base of this layer's root blocks
         uint32_t cnt = N;
 #pragma unroll 1
@@ -1122,20 +1113,19 @@ __global__ __launch_bounds__(512) void k_tree_tail(TailTask tt) {
             }
             if (!level && it == it_root) ch_base = 3u * (ord++), ord++;   // two ordinals (uniform)
             if (chan_wave && job < job_end && (level ? (cnt <= 192 && job < CJ_ROOT) : true)) {
-                chan_job(job, cs, X, has, A, fv, R, FRI_SCHED_CHANNEL ? sl.wk : nullptr, &sl.flag, ch_base);
+                do {
+                    chan_job(job, cs, X, has, A, fv, R, FRI_SCHED_CHANNEL ? sl.wk : nullptr, &sl.flag, ch_base);
 #ifdef FRI_STAMPS
-                if (job >= CJ_ROOT && job <= CJ_ROOT + 2) TAIL_STAMP_T(20 + job - CJ_ROOT, 448, __builtin_amdgcn_s_memrealtime);
+                    if (job >= CJ_ROOT && job <= CJ_ROOT + 2) TAIL_STAMP_T(20 + job - CJ_ROOT, 448, __builtin_amdgcn_s_memrealtime);
 #endif
-                job++;
+                    job++;
+                } while (!level && job < job_end);
             }
             if (FRI_SCHED_CHANNEL && tid >= 384 && tid < 448 && !level && it == it_root) chan_produce(A, &sl, ch_base, R);
             if (coef_late && it == coef_it && tid >= 256 && tid < 384) coef_fold(256, 128);
             if (li == 0 && coef_late && it == coef_it && tid >= 384 && tid < 448) prefetch_x(384, 64);
             lds_barrier();
-            if (coef_late && it == coef_it) {
-                settle(2);
-                total = nlev + (npre_u - pre_in_levels) + (uint32_t)(job_end - CJ_ROOT);
-            }
+            if (coef_late && it == coef_it) settle(2);
             if (level) {
                 uint4* tmp = A; A = B; B = tmp;
                 if (it < 11) TAIL_STAMP(2 + it);
