@@ -719,13 +719,18 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
     uint32_t has = 0, forced = 0, fbeta = 0;
     int job = CJ_END_FINAL;
     if (chan_wave) {
+        // every channel field in one round trip: no load waits on another's
+        // value (the wave reaches the inputs' barrier after this, so a chain
+        // of dependent loads here delays every wave of the launch)
 #pragma unroll
         for (int i = 0; i < 8; i++) cs[i] = st->chan[i];
-        has = st->chan_has;
-        job = !has ? CJ_ROOT : (st->chan_pending ? CJ_REHASH : CJ_MID);
+        const uint32_t h = st->chan_has, pend = st->chan_pending;
         // the test hook's beta, loaded now rather than after the root
-        forced = COMMIT ? st->forced : 0u;
-        if (forced && t.k < MAXR) fbeta = st->forced_beta[t.k];
+        const uint32_t fo = COMMIT ? st->forced : 0u, fb = st->forced_beta[t.k < MAXR ? t.k : 0];
+        has = h;
+        job = !h ? CJ_ROOT : (pend ? CJ_REHASH : CJ_MID);
+        forced = fo;
+        if (fo && t.k < MAXR) fbeta = fb;
     }
     // wave 6 pulls the compact-SHA constant tables into the scalar cache
     // while the inputs load (cold misses inside level 1 and the channel otherwise)
@@ -775,6 +780,10 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
         if ((tid & 63) == 0) { red[3 * (tid >> 6)] = m0; red[3 * (tid >> 6) + 1] = m1; red[3 * (tid >> 6) + 2] = m2; }
     } else {
         const uint32_t* in = tr + 8 * level_offset(L, l);
+        // the producers' maxima are loaded before the digests are waited
+        // for: both round trips overlap (G <= 512 triples, one per thread)
+        int p0 = -1, p1 = -1, p2 = -1;
+        if (COMMIT && tid < G) { p0 = mx[3 * tid]; p1 = mx[3 * tid + 1]; p2 = mx[3 * tid + 2]; }
         for (uint32_t i = tid; i < N; i += blockDim.x) {
             Dg d;
             dg_load(in + 8 * i, d);
@@ -790,8 +799,8 @@ __global__ __launch_bounds__(512) void k_tree_top(LayerTask t, uint32_t l, const
             if ((tid & 63) == 0) { red[3 * (tid >> 6)] = m0; red[3 * (tid >> 6) + 1] = m1; red[3 * (tid >> 6) + 2] = m2; }
         }
         if (COMMIT) {                              // producer maxima -> per-wave triples
-            int m0 = -1, m1 = -1, m2 = -1;
-            for (uint32_t i = tid; i < G; i += blockDim.x) {
+            int m0 = p0, m1 = p1, m2 = p2;
+            for (uint32_t i = tid + blockDim.x; i < G; i += blockDim.x) {
                 m0 = max(m0, mx[3 * i]); m1 = max(m1, mx[3 * i + 1]); m2 = max(m2, mx[3 * i + 2]);
             }
             m0 = wave_max_i(m0); m1 = wave_max_i(m1); m2 = wave_max_i(m2);
