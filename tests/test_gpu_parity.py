@@ -329,6 +329,30 @@ def test_commit_matches_fast_oracle(ctx, corc, oracle, log_n, seed):
     assert bytes(res.channel_out.digest).hex() == och.state.decode()
 
 
+@pytest.mark.parametrize("log_n,d,seed", [(16, 1, 7), (16, 4, 8), (14, 2, 9), (18, 16, 10), (21, 64, 11), (12, 2, 12)])
+def test_commit_final_layer_outside_tail(ctx, corc, oracle, log_n, d, seed):
+    """High blowup: the degree reaches 0 on a layer of >= 2^10 elements, so
+    the final send (channel jobs 6, 7) runs in a k_tree_top after the root
+    (round 5: every post-level job in one iteration), and the tail kernel and
+    later layers are gated off.  Bit-exact against the C oracle."""
+    c = np.array(oracle.splitmix64_field(seed, d), dtype=np.uint64)
+    res = ctx.commit(c, log_n)
+    cs, pc = c_u64(c)
+    och = oracle.OrcChannel()
+    corc.orc_channel_init(ctypes.byref(och))
+    ores = oracle.OrcFriResult()
+    assert corc.orc_fri_commit_fast(pc, d, log_n, 5, 5, P, ctypes.byref(och), None, ctypes.byref(ores),
+                                    None, None) == 0
+    assert log_n - (ores.n_layers - 1) >= 10          # the last layer is not a tail layer
+    assert res.n_layers == ores.n_layers and res.n_rounds == ores.n_rounds
+    for k in range(ores.n_layers):
+        assert bytes(res.roots[k]) == bytes(ores.roots[k])
+    for r in range(ores.n_rounds):
+        assert res.betas[r] == ores.betas[r]
+    assert res.final_value == ores.final_value
+    assert bytes(res.channel_out.digest).hex() == och.state.decode()
+
+
 def test_commit_2p24_full_parity(ctx, corc, oracle):
     """BASELINE config 3 (codeword 2^24, blowup 8): bit-exact against the
     OpenMP C oracle, plus size-independent properties."""
