@@ -1,5 +1,6 @@
 // fri_internal.hpp — device state layout and kernel launchers shared by
-// fri_kernels.hip (kernels) and fri_api.hip (context / C ABI).
+// the kernel files (fri_kernels.hip, fri_layer.hip, ...) and the host code of
+// the C ABI (fri_host.hpp and the files it lists).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>

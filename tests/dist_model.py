@@ -1,6 +1,6 @@
 """CPU model of the coset-sharded FRI commit (test infrastructure).
 
-Mirrors run_commit_sharded (stark-prover_amd/csrc/fri_api.hip) step for step
+Mirrors run_commit_sharded (stark-prover_amd/csrc/fri_sharded.hip) step for step
 with the same index math, using the C oracle for per-block work and
 torch.distributed (gloo) for the exchanges:
 
@@ -70,7 +70,7 @@ def _allgather_records(rec, world):
     return [(roots[r],) + tuple(int(x) for x in outs[r].numpy()) for r in range(world)]
 
 
-def _rounds_bound(d, log_n):                          # fri_api.hip rounds_bound
+def _rounds_bound(d, log_n):                          # fri_host.hpp rounds_bound
     return 0 if d <= 1 else min((d - 1).bit_length(), log_n)
 
 

@@ -72,5 +72,5 @@ def test_source_hash_covers_the_kernels():
     import glob
     files = [f for pat in bench.SOURCE_GLOBS for f in glob.glob(os.path.join(ROOT, pat))]
     names = {os.path.basename(f) for f in files}
-    assert {"fri_layer.hip", "fri_kernels.hip", "fri_api.hip", "sha256_fast.hpp", "fri_amd.h", "Makefile"} <= names
+    assert {"fri_layer.hip", "fri_kernels.hip", "fri_commit.hip", "fri_host.hpp", "sha256_fast.hpp", "fri_amd.h", "Makefile"} <= names
     assert len(bench.source_hash()) == 64

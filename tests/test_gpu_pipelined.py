@@ -380,7 +380,7 @@ def test_input_buffer_read_in_call_order_across_lanes(oracle, oracle_commit, tor
     commit D on lane 1: D must commit what the buffer holds in call order.
     Commits on lane 0 from other pointers stage their coefficients into that
     buffer, so D's copy of it is made on lane 0's stream (commit_enqueue in
-    fri_api.hip): after the stagings of the commits enqueued before D, before
+    fri_lanes.hip): after the stagings of the commits enqueued before D, before
     those of later ones.  Here lane 0 runs two commits that stage a polynomial
     with a coefficient >= p (they stop after layer 0 with FRI_EINVAL) while
     lane 1 runs a whole 2^24 commit B before D; then a synchronous commit

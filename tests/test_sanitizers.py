@@ -11,7 +11,7 @@ the host code of every layer, on the CPU:
   (tests/cpp/test_stark101.cpp), built with -fsanitize=address,undefined
   (stark-prover_amd/Makefile `test_host_asan`), leak detection on;
 * the host code of libfri_amd.so itself (context, commit plans, the shard
-  schedule, argument checks: fri_api.hip compiled with -Xarch_host
+  schedule, argument checks: the C ABI sources compiled with -Xarch_host
   -fsanitize=address,undefined, Makefile `asan`): the plan layout of every
   (world, rank) over a sweep of codewords and degrees, and the no-device /
   bad-argument paths of the C ABI.
@@ -148,7 +148,7 @@ print(json.dumps({"layouts": n, "ctx_rc": rc_ctx}))
 
 
 def test_library_host_code_under_asan_ubsan():
-    """libfri_amd.so's host code (fri_api.hip: commit plans, the coset-shard
+    """libfri_amd.so's host code (fri_*.hip of the C ABI: commit plans, the coset-shard
     schedule of every (world, rank), argument checks) under ASan + UBSan:
     fri_debug_plan_layout over codewords 2^1..2^30 and degree shapes, and the
     no-device paths of the C ABI, without a sanitizer report."""

@@ -1,4 +1,4 @@
-"""CPU: the shard-sized commit plan (fri_api.hip plan_layout, through the
+"""CPU: the shard-sized commit plan (fri_commit.hip plan_layout, through the
 host-only fri_debug_plan_layout; no GPU) against the protocol model.
 
 Each rank of a G-way sharded commit allocates only its block of every sharded

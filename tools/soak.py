@@ -48,7 +48,7 @@ def transcript(r):
 
 class Driven:
     """One context and the model of its state: the result slot of every
-    pending ticket (lowest free slot, fri_api.hip async_enqueue), its lanes,
+    pending ticket (lowest free slot, fri_lanes.hip async_enqueue), its lanes,
     its shape and what its input buffer holds in call order (a pipelined
     commit dealt to lane 0 stages its coefficients there)."""
 
