@@ -52,6 +52,35 @@ def algorithmic_bytes(log_n, d):
     return b_field, 32 * nodes
 
 
+# VALU issue units per SHA-256 compression as the kernels run them (DESIGN.md
+# §5): a leaf hash (one block, message mostly zeros) 2009, an internal node
+# (its block plus the constant padding block) 3592; v_alignbit / v_add3 are
+# half rate on gfx950 and count twice.
+LEAF_ISSUE_UNITS = 2009.0
+NODE_ISSUE_UNITS = 3592.0
+
+
+def valu_issue_units(log_n, d):
+    """Issue units of every leaf and node hash of a whole commit (all R+1
+    layers' trees): the VALU work the commit cannot avoid (1.879e11 at 2^24).
+    NTT, folds and the channel add well under 1%."""
+    rounds = min(max(0, (d - 1).bit_length()), log_n)
+    leaves = sum(1 << (log_n - k) for k in range(rounds + 1))
+    nodes = sum((1 << (log_n - k)) - 1 for k in range(rounds + 1))
+    return leaves * LEAF_ISSUE_UNITS + nodes * NODE_ISSUE_UNITS
+
+
+def whole_commit_valu(log_n, d, ms_per_commit):
+    """valu_issue_units over the time of one commit, against the nominal
+    VALU peak and the measured issue ceiling (the chain's idle chip shows here,
+    where the dominant kernel's own roofline cannot see it)."""
+    units = valu_issue_units(log_n, d)
+    t = units / (ms_per_commit * 1e-3) / 1e12
+    return {"issue_units_per_commit": units, "ms_per_commit": round(ms_per_commit, 4), "achieved": round(t, 2),
+            "unit": "T int32 lane-ops/s", "peak": VALU_PEAK_TOPS, "frac": round(t / VALU_PEAK_TOPS, 4),
+            "measured_ceiling": VALU_MEASURED_TOPS, "frac_of_measured_ceiling": round(t / VALU_MEASURED_TOPS, 4)}
+
+
 def sha_compressions(log_n, d):
     rounds = min(max(0, (d - 1).bit_length()), log_n)
     leaves = sum(1 << (log_n - k) for k in range(rounds + 1))
@@ -392,8 +421,7 @@ def main():
                     note = None
                     ok = ctx.dist_info()[2] != "none"              # an aborted transport ends the sharded run
                 continue
-            dptr = ctypes.c_void_p()
-            ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, dL, ctypes.byref(dptr)))
+            dptr = ctypes.c_void_p(ctx.input_upload(cf))      # inputs resident: this rank's input buffer
             out = fri_amd.CommitResult() if not name.endswith("_primary") else res
 
             def sstep(dptr=dptr, dL=dL, L=L, out=out):
@@ -487,9 +515,9 @@ def main():
         verified = exp is not None and _matches(res0, exp)
         if exp is not None and not verified:
             raise SystemExit("1-GPU transcript differs from the C oracle's (tests/golden/bench_transcripts.json)")
-        # inputs resident in HBM: the plan's input buffer, filled by the untimed first commit
-        dptr = ctypes.c_void_p()
-        ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(dptr)))
+        # inputs resident in HBM: the context's input buffer, filled once
+        # before the timed region (fri_ctx_input_upload) and read in place
+        dptr = ctypes.c_void_p(ctx.input_upload(coeffs))
 
         def step():
             ctx._check(ctx.lib.fri_commit_device(ctx.h, dptr, d, log_n, fri_amd.GENERATOR, None, 0, None,
@@ -614,6 +642,21 @@ def main():
         concurrent["single_thread_async"] = single
     if solo and mode == "single" and log_n >= 20 and not args.no_extras:
         pipelined = _pipelined_stage(fri_amd, ctx, dptr, d, log_n, res0, steps=args.steps)
+    # the whole commit in VALU terms (verdict r05 item 4): the hash work of
+    # every layer over ms_per_step -- what the serial Fiat-Shamir chain costs
+    # shows here, not in the dominant kernel's roofline -- and the same work
+    # over the pipelined per-commit time (commit lanes fill the idle chip)
+    n_dev_valu = (1 << logG) if mode == "sharded" else 1
+    whole["valu"] = whole_commit_valu(log_n, d, ms_per_step)
+    if n_dev_valu > 1:
+        whole["valu"]["n_gpus"] = n_dev_valu
+        whole["valu"]["frac"] = round(whole["valu"]["frac"] / n_dev_valu, 4)
+        whole["valu"]["frac_of_measured_ceiling"] = round(whole["valu"]["frac_of_measured_ceiling"] / n_dev_valu, 4)
+    if pipelined and pipelined.get("ms_per_commit"):
+        whole["valu_pipelined"] = dict(whole_commit_valu(log_n, d, pipelined["ms_per_commit"]),
+                                       lanes=pipelined.get("best_lanes"),
+                                       what="the same work over the per-commit time of the best pipelined_commits "
+                                            "configuration (commits overlapping on commit lanes)")
 
     # PCIe-inclusive rate (host coefficients in, result out): never `value`
     pcie = None
@@ -692,9 +735,15 @@ def main():
     if rank == 0:
         # the sharded run's size as its communicator (or the team) reports it
         n_ranks = (dist_report or {}).get("world_reported", world) if mode == "sharded" else world
+        # GPUs the job actually ran on: fewer than the ranks when ranks share
+        # a device (a rehearsal on a box with fewer GPUs than --gpus); such a
+        # run reports n_gpus = the distinct devices and keeps its points out
+        # of scaling_points
+        n_dev, oversub = devices_used(team_devices if team_n else None, world, ndev_all, n_ranks)
         if mode == "sharded":
             workload = (f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} (d=2^{log_n - args.blowup_log}), "
-                        f"coset-sharded over {n_ranks} GPUs (2^{blk_log} per GPU), SHA-256 Merkle per layer, "
+                        f"coset-sharded over {n_ranks} {'GPUs' if not oversub else f'ranks on {n_dev} GPU(s)'} "
+                        f"(2^{blk_log} per rank), SHA-256 Merkle per layer, "
                         f"{res.n_rounds} rounds")
             if team_n:
                 nd = len(set(team_devices or []))
@@ -713,7 +762,8 @@ def main():
             if fallback:
                 par += f" (FALLBACK: the coset-sharded path failed: {fallback})"
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "field-elems/s", "n_gpus": n_ranks,
+            "metric": METRIC, "value": round(value, 1), "unit": "field-elems/s", "n_gpus": n_dev,
+            "n_ranks": n_ranks,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 % p coefficients" + (", seed 42)" if mode != "replicas" else ", seed 42+rank)"),
@@ -724,7 +774,7 @@ def main():
             "hbm_bytes_per_rank_max": int(hbm_max),
             "roofline": roofline,
             "whole_commit": whole,
-            "scaling_points": secondary or None,
+            "scaling_points": (secondary or None) if not oversub else None,
             "breakdown_ms_per_step": breakdown,
             "pcie_inclusive": pcie,
             "decommit": decommit,
@@ -737,6 +787,12 @@ def main():
         }
         if fallback:
             line["note"] = fallback
+        if oversub:
+            line["oversubscribed"] = True
+            line["rehearsal_points"] = secondary or None
+            line["note"] = ((line.get("note") + "; ") if line.get("note") else "") + (
+                f"OVERSUBSCRIBED: {n_ranks} ranks on {n_dev} device(s): a correctness/rehearsal run, "
+                f"not a {n_ranks}-GPU scaling point")
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     if mode == "sharded" and not team_n:
         ctx.detach()
@@ -745,6 +801,16 @@ def main():
         dist.destroy_process_group()
     elif pg is not None:
         _team_wait(pg)                   # the ranks that waited for this team run
+
+
+def devices_used(team_devices, world, ndev, n_ranks):
+    """(distinct GPUs the job ran on, whether ranks share them): a team's
+    device list, else one process per rank on local_rank % ndev."""
+    if team_devices is not None:
+        n_dev = len(set(team_devices)) or 1
+    else:
+        n_dev = min(world, max(ndev, 1)) if world > 1 else 1
+    return n_dev, n_ranks > n_dev
 
 
 def _device_count():
@@ -804,11 +870,13 @@ def _team_stage(fri_amd, devices, points, args, timed):
         dL = 1 << (L - args.blowup_log)
         cf = _coeffs(42, dL, fri_amd.P)
         exp = _expected(L, args.blowup_log)
-        first = ctx.commit(cf, L)
+        first = ctx.commit(cf, L)          # host input: every rank stages it (ranks 1..G-1: their copies)
         if exp is not None and not _matches(first, exp):
             raise RuntimeError(f"team transcript of 2^{L} differs from the C oracle's")
-        dptr = ctypes.c_void_p()
-        ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, dL, ctypes.byref(dptr)))
+        # rank 0's input buffer gets the same coefficients; the timed steps
+        # reuse the ranks' staged copies (FRI_FLAG_RANK_INPUTS, verified by a
+        # per-rank checksum against this buffer on every step)
+        dptr = ctypes.c_void_p(ctx.input_upload(cf))
         res = fri_amd.CommitResult()
 
         def step(dptr=dptr, dL=dL, L=L, res=res):
@@ -879,8 +947,7 @@ def _concurrent_stage(fri_amd, ctx, dptr, d, log_n, res0, C, steps):
     for c in range(1, C):
         cx = fri_amd.Context(ctx_device(ctx), log_n)
         cx.commit(_coeffs(seeds[c], d, fri_amd.P), log_n)
-        p = ctypes.c_void_p()
-        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p)))
+        p = ctypes.c_void_p(cx.input_upload(_coeffs(seeds[c], d, fri_amd.P)))
         ctxs.append(cx)
         ptrs.append(p)
 
@@ -1023,8 +1090,7 @@ def _concurrent_async_stage(fri_amd, ctx, dptr, d, log_n, res0, K, steps, depth=
     for j in range(1, K):
         cx = fri_amd.Context(ctx_device(ctx), log_n)
         cx.commit(_coeffs(seeds[j], d, fri_amd.P), log_n)
-        p = ctypes.c_void_p()
-        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p)))
+        p = ctypes.c_void_p(cx.input_upload(_coeffs(seeds[j], d, fri_amd.P)))
         ctxs.append(cx)
         ptrs.append(p)
 
@@ -1164,8 +1230,7 @@ def _single_point(fri_amd, device, log_n, blowup_log, steps):
     try:
         r0 = cx.commit(_coeffs(42, d, fri_amd.P), log_n)
         exp = _expected(log_n, blowup_log)
-        p = ctypes.c_void_p()
-        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p)))
+        p = ctypes.c_void_p(cx.input_upload(_coeffs(42, d, fri_amd.P)))
         r = fri_amd.CommitResult()
 
         def st():

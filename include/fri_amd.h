@@ -78,12 +78,16 @@ typedef struct fri_ctx fri_ctx;
                                      channel's draw (transcript still absorbs roots) */
 #define FRI_FLAG_NO_GRAPH    2u   /* run eagerly instead of replaying a hipGraph   */
 #define FRI_FLAG_RANK_INPUTS 4u   /* multi-GPU context, fri_commit_device with
-                                     fri_ctx_input_buffer(): every rank's own input
-                                     buffer already holds these coefficients (it
-                                     does after any team commit of them, until the
-                                     caller rewrites rank 0's buffer), so no rank
-                                     copies rank 0's over xGMI; FRI_ESTATE when a
-                                     rank has no input buffer of this shape yet */
+                                     fri_ctx_input_buffer(): ranks 1..n-1 commit the
+                                     copy of rank 0's buffer their plan staged at the
+                                     last team commit of this shape instead of
+                                     copying it again over xGMI.  Verified, not
+                                     trusted: every rank hashes the input it would
+                                     commit (a position-sensitive 64-bit checksum)
+                                     and the call returns FRI_ESTATE, committing
+                                     nothing, when a rank's copy differs from rank
+                                     0's buffer (rewritten since it was staged) or
+                                     no copy of this shape was staged yet */
 
 /* ---------------------------------------------------------------- context */
 /* Opens `device` (HIP ordinal) and sizes scratch for codewords up to
@@ -208,15 +212,22 @@ int fri_commit_device(fri_ctx* ctx, const uint32_t* d_coeffs, size_t d, uint32_t
                       uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                       const uint32_t* forced_betas, fri_commit_result* out);
 
-/* Device buffer of >= d words owned by the context that fri_commit_device
- * reads without a copy (commit lane 0's input buffer; synchronous commits run
- * on lane 0).  Valid until the next commit with another (d, log_n, offset).
- * A commit on lane 0 from any other device or host pointer copies its
- * coefficients into this buffer; a pipelined commit on another lane that is
- * handed this buffer copies it into its own lane's buffer on lane 0's stream,
- * so it reads the contents in call order (what the commits enqueued before it
- * staged there, not what later ones stage). */
+/* The context's input buffer: a device buffer of >= d words (on rank 0's
+ * device for a multi-GPU context) that fri_commit_device and
+ * fri_commit_device_async read in place, on any commit lane, without a copy.
+ * It belongs to the caller, as `poly` does in fri_commit(poly, domain,
+ * &mut channel) (src/fri/fri_commit.rs:72-76): no commit ever writes it, so a
+ * commit from it commits exactly what the caller last wrote there (with its
+ * own kernels or copies, or fri_ctx_input_upload), whatever was committed
+ * before or on which lane.  Commits from any other pointer stage their
+ * coefficients in the plan's private buffer instead.  Created on first call;
+ * valid until a call with a larger d moves it (contents kept) or
+ * fri_ctx_destroy.  d <= 2^log_n_max. */
 int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
+/* Fills the input buffer (grown to >= d words as fri_ctx_input_buffer does)
+ * with d host coefficients, after the pending pipelined commits that read it
+ * have finished; returns when the copy is complete. */
+int fri_ctx_input_upload(fri_ctx* ctx, const uint32_t* coeffs, size_t d);
 
 /* Pipelined commits: a prover that commits many codewords in a row calls
  * fri_commit (src/fri/fri_commit.rs:72-122) in a loop; here it enqueues them.
@@ -232,10 +243,9 @@ int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr);
  * commit and wait for it.  Not while profiling (FRI_ESTATE).
  * d_coeffs is read when the commit runs on the device, not when the call
  * returns: it must stay unchanged until fri_commit_wait(ticket) has returned.
- * fri_ctx_input_buffer() is one buffer shared by every pending commit of the
- * context, so refilling it yourself while a commit that reads it is pending
- * commits the new contents (the context's own stagings into it are ordered,
- * see fri_ctx_input_buffer); give each pending commit its own device buffer, or use
+ * fri_ctx_input_buffer() is one buffer, read in place by every pending commit
+ * handed it: refill it only through fri_ctx_input_upload (which waits for
+ * them), give each pending commit its own device buffer, or use
  * fri_commit_async, which copies host coefficients into the ticket's own
  * pinned buffer before returning. */
 #define FRI_MAX_INFLIGHT 4
@@ -316,11 +326,17 @@ int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t va
  * 1 gives an ordinary context.  log_n_max: the largest codeword; every
  * rank's context is shard-sized (2^(log_n_max - log2 n), and at least
  * 2^min(log_n_max, 19) for the commits rank 0 runs alone).  transport:
- *   FRI_TRANSPORT_RCCL  communicators from ncclCommInitAll (xGMI);
  *   FRI_TRANSPORT_PEER  device copies between the ranks' buffers: one pull
  *                       kernel per collective reading the other ranks'
- *                       memory over xGMI peer access, ordered by events;
- *   FRI_TRANSPORT_NONE  automatic: RCCL when it initialises, else peer.
+ *                       memory over xGMI peer access (hipMemcpyPeerAsync per
+ *                       source where peer access is unavailable), ordered by
+ *                       events;
+ *   FRI_TRANSPORT_NONE  the default: the peer transport;
+ *   FRI_TRANSPORT_RCCL  opt-in: communicators from ncclCommInitAll (xGMI),
+ *                       distinct devices only (FRI_EINVAL otherwise).  A rank
+ *                       that fails aborts its communicators at once and the
+ *                       others theirs when they see it (FRI_ERCCL); the
+ *                       team's later sharded calls then return FRI_ESTATE.
  * Inside, rank 0 runs on the calling thread and ranks 1..n-1 on worker
  * threads of the context (one per rank), each issuing the sharded protocol
  * of fri_commit_sharded on its device.  The returned context is rank 0's:
@@ -339,6 +355,19 @@ int fri_decommit_query(fri_ctx* ctx, uint64_t index, uint32_t* values, size_t va
  * Not re-entrant (one host thread at a time), like every context.
  * fri_ctx_destroy(ctx) releases every rank. */
 int fri_ctx_create_multi(const int* devices, uint32_t n_devices, uint32_t log_n_max, int transport, fri_ctx** out);
+/* The context a caller gets without naming devices -- what a binding that
+ * keeps the reference's signatures (fri_commit(poly, domain, &mut channel),
+ * decommit_fri(num_queries, max_index, &layers, &merkles, &mut channel);
+ * src/fri/fri_commit.rs:72-76,168-174) opens behind them: the devices are
+ *   FRI_DEVICES  (environment) comma-separated HIP ordinals, a power-of-two
+ *                count <= 64, ordinals may repeat (e.g. "0,0,0,0": four
+ *                ranks on one GPU);
+ *   otherwise    0..k-1, k the largest power of two <= the visible devices;
+ * one device gives fri_ctx_create, several fri_ctx_create_multi with the
+ * transport FRI_TRANSPORT (environment: "peer", the default, or "rccl").
+ * *n_ranks (may be NULL) = the number of ranks.  FRI_EINVAL for a malformed
+ * FRI_DEVICES or FRI_TRANSPORT. */
+int fri_ctx_create_default(uint32_t log_n_max, fri_ctx** out, uint32_t* n_ranks);
 /* Diagnostic: rank `rank`'s context of a team (rank 0: ctx itself), e.g. for
  * its fri_debug_transport_log; owned by the team, never destroyed by the
  * caller (FRI_EINVAL). */
@@ -346,8 +375,14 @@ int fri_debug_team_rank(fri_ctx* ctx, uint32_t rank, fri_ctx** out);
 /* Test hook (peer transport): the next team call makes rank `rank` fail
  * with FRI_ERCCL at its op_index-th collective (0-based), as a rank whose
  * transfer broke would; the other ranks must return instead of waiting for
- * it.  Fires once; op_index < 0 clears it. */
+ * it.  Applies to the next team call only (cleared at its end, fired or
+ * not); op_index < 0 clears it. */
 int fri_debug_team_inject_failure(fri_ctx* ctx, uint32_t rank, int64_t op_index);
+/* Test hook (peer transport): enable != 0 makes every collective copy with
+ * hipMemcpyPeerAsync per source, the path a team takes when peer access is
+ * unavailable, instead of the pull kernel; 0 restores the pull kernel where
+ * peer access allows it. */
+int fri_debug_team_force_copy(fri_ctx* ctx, int enable);
 
 /* -------------------------------------------------------------- multi-GPU */
 /* One process per GPU.  A codeword of 2^log_n is committed by G ranks

@@ -130,14 +130,10 @@ int fri::plan_build(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset, uin
     return FRI_OK;
 }
 
-static const uint32_t* root_ptr(const Plan& p, int k) {
-    uint32_t L = p.log_n - (uint32_t)k;
-    return p.trees + p.tree_off[k] + 8 * level_offset(L, L);
-}
-
-// poly_r coefficient buffer: poly_0 is the input, then A/B alternate.
+// poly_r coefficient buffer: poly_0 is the commit's input (p.src, only ever
+// read), then A/B alternate.
 uint32_t* fri::coef_buf(Plan& p, int r) {
-    if (r == 0) return p.d_in;
+    if (r == 0) return const_cast<uint32_t*>(p.src);
     return (r % 2 == 1) ? p.coefA : p.coefB;
 }
 
@@ -151,7 +147,7 @@ LayerTask fri::commit_task(fri_ctx* ctx, int k) {
     t.tree = p.trees + p.tree_off[k];
     t.L = p.log_n - (uint32_t)k;
     t.k = k;
-    t.coef_in = k ? coef_buf(p, k - 1) : p.d_in;
+    t.coef_in = coef_buf(p, k ? k - 1 : 0);
     t.coef_out = k ? coef_buf(p, k) : nullptr;
     t.d0 = p.d;
     t.wgmax = p.wgmax;
@@ -171,7 +167,7 @@ static void enqueue_commit(fri_ctx* ctx) {
     np.pre_hi = p.pre_hi;
     np.scratch = p.trees;                 // free until layer 0's leaf kernel (>= 16n words)
     size_t sp = span_begin(ctx, "lde", p.d * 4 + n * 4);
-    launch_ntt(np, p.d_in, p.d, p.layers + p.layer_off[0], s);
+    launch_ntt(np, p.src, p.d, p.layers + p.layer_off[0], s);
     span_end(ctx, sp);
     for (int k = 0; k <= p.rmax; k++) {
         const uint32_t L = log_n - (uint32_t)k;
@@ -185,18 +181,7 @@ static void enqueue_commit(fri_ctx* ctx) {
             span_end(ctx, spk);
             break;
         }
-        LayerTask t{};
-        t.prev = k ? p.layers + p.layer_off[k - 1] : nullptr;
-        t.xinv = k ? p.xinv + p.xinv_off[k - 1] : nullptr;
-        t.values = p.layers + p.layer_off[k];
-        t.tree = p.trees + p.tree_off[k];
-        t.L = L;
-        t.k = k;
-        t.coef_in = k ? coef_buf(p, k - 1) : p.d_in;
-        t.coef_out = k ? coef_buf(p, k) : nullptr;
-        t.d0 = p.d;
-        t.wgmax = p.wgmax;
-        t.st = ctx->d_state;
+        const LayerTask t = commit_task(ctx, k);
         // Algorithmic bytes of layer 0's leaf kernel: read the values and the
         // input coefficients (degree scan), write tree levels 0..4.
         uint64_t leaf_nodes = 0;
@@ -249,11 +234,6 @@ int fri::commit_validate(fri_ctx* ctx, size_t d, uint32_t log_n, uint32_t offset
     return FRI_OK;
 }
 
-// 0 only in a diagnostic build (tests/test_gpu_pipelined.py shows the race it closes)
-#ifndef FRI_LANE0_INPUT_ORDERED
-#define FRI_LANE0_INPUT_ORDERED 1
-#endif
-
 int fri::commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_coeffs, size_t d,
                           uint32_t log_n, uint32_t offset, const fri_channel_state* chan_in, uint32_t flags,
                           const uint32_t* forced_betas, int slot) {
@@ -268,36 +248,37 @@ int fri::commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_
     DevState* hs = slot < 0 ? ctx->h_sync : ctx->h_slot[slot];
     init_state(ctx, hs, chan_in, flags, forced_betas);
     ctx->commit_log_n = log_n;
-    const Lane& l0 = ctx->lanes[0];
-    if (FRI_LANE0_INPUT_ORDERED && slot >= 0 && ctx->cur_lane != 0 && d && dev_coeffs && l0.plan.valid &&
-        dev_coeffs == l0.plan.d_in) {
-        // Lane 0's input buffer (fri_ctx_input_buffer) handed to a commit on
-        // another lane.  Every commit on lane 0 from another pointer stages its
-        // coefficients into that buffer on lane 0's stream, so the copy is made
-        // there too: it reads what the buffer holds in call order (after the
-        // stagings of commits enqueued before this one, before those of later
-        // ones), and this lane's stream waits for it.
-        // The copy overwrites this lane's own input buffer, which the commits
-        // already queued on this lane may still read: lane 0's stream first
-        // waits for them (the event is re-recorded after the copy; each wait
-        // binds to the record before it).
-        if (!ctx->ev_src[slot]) FRI_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_src[slot], hipEventDisableTiming));
-        FRI_HIP(ctx, hipEventRecord(ctx->ev_src[slot], s));
-        FRI_HIP(ctx, hipStreamWaitEvent(l0.stream, ctx->ev_src[slot], 0));
-        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, l0.stream));
-        FRI_HIP(ctx, hipEventRecord(ctx->ev_src[slot], l0.stream));
-        FRI_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_src[slot], 0));
-    } else if (host_coeffs && d) {
-        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
-    } else if (dev_coeffs && dev_coeffs != p.d_in && d) {
-        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, s));
+    // The input.  The context's input buffer (fri_ctx_input_buffer) is read
+    // in place, on whichever lane: nothing but the caller (or
+    // fri_ctx_input_upload) writes it, so a commit reads what the caller put
+    // there, whatever was committed before.  Any other input is staged into
+    // this plan's private buffer on this lane's stream.
+    if (dev_coeffs && d && ctx->user_in && dev_coeffs == ctx->user_in) {
+        p.src = ctx->user_in;
+    } else {
+        if (host_coeffs && d)
+            FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
+        else if (dev_coeffs && d && dev_coeffs != p.d_in)
+            FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDeviceToDevice, s));
+        p.src = p.d_in;
     }
     const bool use_graph = !(flags & FRI_FLAG_NO_GRAPH) && !ctx->profiling;
     if (use_graph) {
         // the DevState copies in (from the pinned state just written) and out
-        // are nodes of the graph: no host API call between the commits' kernels
-        hipGraph_t& pg = slot < 0 ? p.graph : p.slot_graph[slot];
-        hipGraphExec_t& px = slot < 0 ? p.exec : p.slot_exec[slot];
+        // are nodes of the graph: no host API call between the commits' kernels.
+        // One graph per (result slot, input): the input pointer is baked into
+        // the LDE and coefficient launches.
+        const int gs = slot < 0 ? FRI_MAX_INFLIGHT : slot;
+        const int gv = p.src == p.d_in ? 0 : 1;
+        hipGraph_t& pg = p.graph[gs][gv];
+        hipGraphExec_t& px = p.exec[gs][gv];
+        if (px && p.graph_src[gs][gv] != p.src) {       // the caller's buffer moved (a larger d)
+            FRI_HIP(ctx, hipStreamSynchronize(s));         // (the old graph may still be running)
+            hipGraphExecDestroy(px);
+            hipGraphDestroy(pg);
+            px = nullptr;
+            pg = nullptr;
+        }
         if (!px) {
             FRI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             // a failure inside the capture still ends it (the stream must not
@@ -315,6 +296,7 @@ int fri::commit_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_
             }
             pg = g;
             FRI_HIP(ctx, hipGraphInstantiate(&px, g, nullptr, nullptr, 0));
+            p.graph_src[gs][gv] = p.src;
         }
         FRI_HIP(ctx, hipGraphLaunch(px, s));
     } else {
@@ -354,8 +336,8 @@ int fri::run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* d
     // the resident commit on its own lane, see settle)
     int rc = commit_validate(ctx, d, log_n, offset, flags, forced_betas);
     if (rc) return rc;
-    // synchronous commits run on lane 0, whose input buffer is the one
-    // fri_ctx_input_buffer hands out (after any commit pending on that lane)
+    // synchronous commits run on lane 0 (always built: the fallback lane of
+    // the pipelined commits, fri_lanes.hip)
     rc = use_lane(ctx, 0);
     if (rc) return rc;
     rc = commit_enqueue(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, -1);

@@ -124,11 +124,13 @@ extern "C" int fri_ctx_destroy(fri_ctx* ctx) {
     if (ctx->interp_tmp) dfree(ctx, ctx->interp_tmp);
     dfree(ctx, ctx->trace_tree);
     dfree(ctx, ctx->trace_lde);
+    dfree(ctx, ctx->user_in);
+    dfree(ctx, ctx->d_csum);
+    if (ctx->h_csum) hipHostFree(ctx->h_csum);
     if (ctx->h_sync) hipHostFree(ctx->h_sync);
     for (int i = 0; i < FRI_MAX_INFLIGHT; i++) {
         if (ctx->h_slot[i]) hipHostFree(ctx->h_slot[i]);
         if (ctx->ev_slot[i]) hipEventDestroy(ctx->ev_slot[i]);
-        if (ctx->ev_src[i]) hipEventDestroy(ctx->ev_src[i]);
         if (ctx->h_in[i]) hipHostFree(ctx->h_in[i]);
         dfree(ctx, ctx->d_slot_in[i]);
         if (ctx->ev_in[i]) hipEventDestroy(ctx->ev_in[i]);

@@ -140,4 +140,36 @@ void launch_peer_pull(const PeerPull& pp, hipStream_t s) {
     hipLaunchKernelGGL(k_peer_pull, dim3(gx, pp.n), dim3(256), 0, s, pp);
 }
 
+// Input checksum (FRI_FLAG_RANK_INPUTS: every rank's resident input must be
+// rank 0's buffer): the wrapping 64-bit sum over i of mix(i << 32 | v[i]),
+// mix = the splitmix64 finaliser.  Order- and position-sensitive, so a
+// rewritten, shifted or truncated input changes it with probability
+// 1 - 2^-64 per change; one atomic per workgroup (a vector global atomic).
+__device__ inline uint64_t csum_mix(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+__global__ __launch_bounds__(256) void k_checksum(const uint32_t* __restrict__ v, size_t n,
+                                                  unsigned long long* out) {
+    __shared__ uint64_t part[256];
+    uint64_t acc = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        acc += csum_mix(((uint64_t)i << 32) | v[i]);
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)part[0]);
+}
+void launch_checksum(const uint32_t* v, size_t n, uint64_t* out, hipStream_t s) {
+    (void)hipMemsetAsync(out, 0, sizeof(uint64_t), s);
+    const unsigned blocks = (unsigned)std::min<size_t>(1024, std::max<size_t>(1, (n + 2047) / 2048));
+    hipLaunchKernelGGL(k_checksum, dim3(blocks), dim3(256), 0, s, v, n, reinterpret_cast<unsigned long long*>(out));
+}
+
 }  // namespace fri

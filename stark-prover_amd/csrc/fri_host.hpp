@@ -62,7 +62,12 @@ struct Plan {
     // coefF receives poly_{k_sw} whole at the switch to the local tail.
     uint32_t cs0 = 0;
     uint32_t* coefF = nullptr;  size_t coefF_cap = 0;
+    // The commit's input: d_in is the plan's private staging buffer (host
+    // coefficients and other device pointers are copied there); src is what
+    // the launch sequence of the commit being enqueued reads: d_in, or the
+    // context's caller-owned input buffer (fri_ctx::user_in), read in place.
     uint32_t* d_in = nullptr;   size_t in_cap = 0;
+    const uint32_t* src = nullptr;
     uint32_t* coefA = nullptr;
     uint32_t* coefB = nullptr;  size_t coef_cap = 0;
     uint32_t* layers = nullptr; size_t layer_off[MAXR + 2] = {0};
@@ -73,10 +78,13 @@ struct Plan {
     uint32_t* pre_lo = nullptr;
     uint32_t* pre_hi = nullptr;
     int32_t* wgmax = nullptr;       // per-workgroup coefficient maxima
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    hipGraph_t slot_graph[FRI_MAX_INFLIGHT] = {};       // fri_commit_device_async: one graph per result slot
-    hipGraphExec_t slot_exec[FRI_MAX_INFLIGHT] = {};    // (the DevState copy-out node targets the slot)
+    // Commit graphs: one per (result slot, input), the synchronous commit's
+    // as slot FRI_MAX_INFLIGHT (the DevState copy-out node targets the slot);
+    // input 0 reads d_in, input 1 the caller's buffer at graph_src (captured
+    // again when that buffer moves).
+    hipGraph_t graph[FRI_MAX_INFLIGHT + 1][2] = {};
+    hipGraphExec_t exec[FRI_MAX_INFLIGHT + 1][2] = {};
+    const uint32_t* graph_src[FRI_MAX_INFLIGHT + 1][2] = {};
     hipGraph_t tail_graph = nullptr;        // sharded plan: the local layers after the switch
     hipGraphExec_t tail_exec = nullptr;
     bool graph_profiled = false;
@@ -153,7 +161,9 @@ struct Team {
     int kind = FRI_TRANSPORT_PEER;          // FRI_TRANSPORT_PEER or FRI_TRANSPORT_RCCL
     std::vector<int> dev;
     std::vector<fri_ctx*> rk;               // rk[0] = the owning context
-    bool kernel_pull = true;                // every device can read every other's memory
+    bool can_pull = true;                   // every device can read every other's memory (peer access)
+    bool kernel_pull = true;                // peer_op pulls with k_peer_pull (else hipMemcpyPeerAsync)
+    std::vector<std::pair<int, int>> peer_pairs;   // device pairs whose peer access this team holds
     // job dispatch to the worker threads (ranks 1..G-1)
     std::vector<std::thread> th;
     std::mutex jm;
@@ -202,9 +212,7 @@ struct fri_ctx {
     uint64_t slot_ticket[FRI_MAX_INFLIGHT] = {};
     uint32_t slot_log_n[FRI_MAX_INFLIGHT] = {};
     bool slot_pending[FRI_MAX_INFLIGHT] = {};
-    // a pipelined commit on another lane handed lane 0's input buffer: its
-    // copy of that buffer, made on lane 0's stream, ends with this event
-    hipEvent_t ev_src[FRI_MAX_INFLIGHT] = {};
+    bool slot_user[FRI_MAX_INFLIGHT] = {};   // pending slot i reads user_in (fri_ctx_input_upload waits for it)
     uint32_t* h_in[FRI_MAX_INFLIGHT] = {};  // fri_commit_async: pinned copy of the slot's host coefficients,
     uint32_t* d_slot_in[FRI_MAX_INFLIGHT] = {};   // its device copy (uploaded on h2d_stream while the
     size_t h_in_cap[FRI_MAX_INFLIGHT] = {};       // previous commit runs) and the upload's event
@@ -251,6 +259,13 @@ struct fri_ctx {
     size_t dev_bytes = 0, dev_peak = 0;
     size_t dev_cap = 0;             // fri_debug_set_device_cap: allocations beyond it fail (0: none)
     Team* team_root = nullptr;      // fri_ctx_create_multi: this context is rank 0 and owns the team
+    // The caller-owned input buffer (fri_ctx_input_buffer): written only by the
+    // caller or by fri_ctx_input_upload, never by a commit; commits from it
+    // read it in place, on any lane.
+    uint32_t* user_in = nullptr;
+    size_t user_cap = 0;
+    uint64_t* d_csum = nullptr;     // input checksum (FRI_FLAG_RANK_INPUTS): device word ...
+    uint64_t* h_csum = nullptr;     // ... and its pinned host copy
 };
 
 namespace fri {
@@ -408,6 +423,8 @@ int run_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* dev_co
 
 // ---- fri_readback.hip
 int dq_alloc(fri_ctx* ctx);                   // pinned host buffer the gather kernels write
+
+int input_checksum(fri_ctx* ctx, const uint32_t* d_src, size_t d, uint64_t* out);   // (synchronous)
 
 // ---- fri_transport.hip
 int tp_host_stage(fri_ctx* ctx, size_t bytes);

@@ -201,6 +201,8 @@ struct PeerPull {
     uint32_t vec4;
 };
 void launch_peer_pull(const PeerPull& pp, hipStream_t s);
+// *out = position-sensitive 64-bit checksum of v[0..n) (FRI_FLAG_RANK_INPUTS).
+void launch_checksum(const uint32_t* v, size_t n, uint64_t* out, hipStream_t s);
 // Loopback rehearsal: dst = G copies of src (words each), one launch.
 void launch_replicate(const uint32_t* src, uint32_t* dst, size_t words, uint32_t G, hipStream_t s);
 // Tree top + degree + channel step for a layer whose level `l` (2^(L-l)

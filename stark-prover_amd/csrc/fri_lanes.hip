@@ -5,12 +5,11 @@
 
 // Free one plan's buffers and graphs (its lane's stream must be idle).
 void fri::plan_release(fri_ctx* ctx, Plan& p) {
-    if (p.exec) hipGraphExecDestroy(p.exec);
-    if (p.graph) hipGraphDestroy(p.graph);
-    for (int i = 0; i < FRI_MAX_INFLIGHT; i++) {
-        if (p.slot_exec[i]) hipGraphExecDestroy(p.slot_exec[i]);
-        if (p.slot_graph[i]) hipGraphDestroy(p.slot_graph[i]);
-    }
+    for (int i = 0; i <= FRI_MAX_INFLIGHT; i++)
+        for (int v = 0; v < 2; v++) {
+            if (p.exec[i][v]) hipGraphExecDestroy(p.exec[i][v]);
+            if (p.graph[i][v]) hipGraphDestroy(p.graph[i][v]);
+        }
     if (p.tail_exec) hipGraphExecDestroy(p.tail_exec);
     if (p.tail_graph) hipGraphDestroy(p.tail_graph);
     dfree(ctx, p.d_in); dfree(ctx, p.coefA); dfree(ctx, p.coefB); dfree(ctx, p.coefF); dfree(ctx, p.layers);
@@ -170,6 +169,7 @@ static int async_enqueue(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32
     }
     FRI_HIP(ctx, hipEventRecord(ctx->ev_slot[slot], ctx->stream));
     ctx->slot_pending[slot] = true;
+    ctx->slot_user[slot] = ctx->plan.src == ctx->user_in;     // reads the caller's buffer in place
     ctx->slot_lane[slot] = ctx->cur_lane;
     ctx->lane_ticket[ctx->cur_lane] = ctx->next_ticket;
     ctx->slot_ticket[slot] = ctx->next_ticket++;
@@ -200,6 +200,7 @@ extern "C" int fri_commit_wait(fri_ctx* ctx, uint64_t ticket, fri_commit_result*
         if (ctx->slot_pending[i] && ctx->slot_ticket[i] == ticket) slot = i;
     if (slot < 0) return fail(ctx, FRI_EINVAL, "no pending commit with this ticket");
     ctx->slot_pending[slot] = false;
+    ctx->slot_user[slot] = false;
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     FRI_HIP(ctx, hipEventSynchronize(ctx->ev_slot[slot]));
     return commit_finish(ctx, ctx->h_slot[slot], ctx->slot_log_n[slot], out);
@@ -225,16 +226,79 @@ extern "C" int fri_debug_ticket_lane(fri_ctx* ctx, uint64_t ticket, int* lane) {
     return fail(ctx, FRI_EINVAL, "no pending commit with this ticket");
 }
 
+// ---- the caller-owned input buffer --------------------------------------
+// The pending pipelined commits that read the input buffer in place have
+// finished (before it is refilled by fri_ctx_input_upload or moved).
+static int wait_user_readers(fri_ctx* ctx) {
+    for (int i = 0; i < FRI_MAX_INFLIGHT; i++)
+        if (ctx->slot_pending[i] && ctx->slot_user[i]) FRI_HIP(ctx, hipEventSynchronize(ctx->ev_slot[i]));
+    return FRI_OK;
+}
+
+// One buffer per context (rank 0's device on a team), independent of the
+// commit plans: the reference's caller owns `poly` (fri_commit.rs:72-76), and
+// so does the caller here.  No commit writes it; a commit from it reads it in
+// place on any lane, so what a commit commits is what the caller last wrote
+// there, whatever the lane deal or the commits before it did.
 extern "C" int fri_ctx_input_buffer(fri_ctx* ctx, size_t d, uint32_t** d_ptr) {
     if (!ctx || !d_ptr) return fail(ctx, FRI_EINVAL, "null argument");
-    // The plan's input buffer is only stable for a fixed (d, log_n, offset);
-    // the caller passes the returned pointer back to fri_commit_device, which
-    // skips the copy when the pointers match.
-    // lane 0's (synchronous commits run there; pipelined commits on other
-    // lanes copy from it into their own input buffers)
-    const Plan& p0 = ctx->cur_lane == 0 ? ctx->plan : ctx->lanes[0].plan;
-    if (!p0.valid || p0.d != d) return fail(ctx, FRI_ESTATE, "build a plan first (commit once with this d)");
-    *d_ptr = p0.d_in;
+    if (d > ((size_t)1 << ctx->log_n_max)) return fail(ctx, FRI_EINVAL, "d exceeds the context's codeword bound");
+    const size_t want = d ? d : 1;
+    if (ctx->user_cap < want) {
+        // a larger buffer: the commits still reading the old one finish first
+        // (its graphs are captured again on their next use, fri_commit.hip)
+        FRI_HIP(ctx, hipSetDevice(ctx->device));
+        int rc = wait_user_readers(ctx);
+        if (rc) return rc;
+        FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        uint32_t* nb = nullptr;
+        if (dalloc(ctx, &nb, want * 4) != hipSuccess) return fail(ctx, FRI_ENOMEM, "input buffer");
+        if (ctx->user_in) {
+            // the old contents move along (the caller may have filled it for
+            // a smaller d); on the context stream, not the null stream
+            const hipError_t e1 = hipMemcpyAsync(nb, ctx->user_in, ctx->user_cap * 4, hipMemcpyDeviceToDevice,
+                                                 ctx->stream);
+            const hipError_t e2 = e1 == hipSuccess ? hipStreamSynchronize(ctx->stream) : e1;
+            if (e2 != hipSuccess) {
+                dfree(ctx, nb);
+                FRI_HIP(ctx, e2);
+            }
+            dfree(ctx, ctx->user_in);
+        }
+        ctx->user_in = nb;
+        ctx->user_cap = want;
+    }
+    *d_ptr = ctx->user_in;
+    return FRI_OK;
+}
+
+extern "C" int fri_ctx_input_upload(fri_ctx* ctx, const uint32_t* coeffs, size_t d) {
+    if (!ctx || (d && !coeffs)) return fail(ctx, FRI_EINVAL, "null argument");
+    uint32_t* buf = nullptr;
+    int rc = fri_ctx_input_buffer(ctx, d, &buf);
+    if (rc) return rc;
+    if (!d) return FRI_OK;
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    if ((rc = wait_user_readers(ctx))) return rc;
+    // on the context stream (not the null stream, which would hold a hardware
+    // queue of its own), ordered after every commit queued there
+    FRI_HIP(ctx, hipMemcpyAsync(buf, coeffs, d * 4, hipMemcpyHostToDevice, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return FRI_OK;
+}
+
+int fri::input_checksum(fri_ctx* ctx, const uint32_t* d_src, size_t d, uint64_t* out) {
+    FRI_HIP(ctx, hipSetDevice(ctx->device));
+    if (!ctx->d_csum && dalloc(ctx, &ctx->d_csum, 64) != hipSuccess) {
+        ctx->d_csum = nullptr;
+        return fail(ctx, FRI_ENOMEM, "checksum word");
+    }
+    if (!ctx->h_csum) FRI_HIP(ctx, hipHostMalloc(&ctx->h_csum, 64, hipHostMallocDefault));
+    launch_checksum(d_src, d, ctx->d_csum, ctx->stream);
+    FRI_HIP(ctx, hipGetLastError());
+    FRI_HIP(ctx, hipMemcpyAsync(ctx->h_csum, ctx->d_csum, sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *out = *ctx->h_csum;
     return FRI_OK;
 }
 

@@ -37,10 +37,14 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
     ctx->sharded_layers = (uint32_t)p.rmax + 1;      // lowered when the tail goes local
     init_state(ctx, ctx->h_sync, chan_in, flags, forced_betas);
     FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
+    // the input is always staged into the plan's own buffer (rank 0 of a team
+    // copies the caller's buffer locally, ranks 1..G-1 over xGMI), so the
+    // launches below and the local tail's graph read one fixed pointer
     if (host_coeffs && d)
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
     else if (dev_coeffs && dev_coeffs != p.d_in && d)   // (Default: a team rank reads rank 0's device buffer)
         FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDefault, s));
+    p.src = p.d_in;
 
     size_t sp;
     if (G == 2) {

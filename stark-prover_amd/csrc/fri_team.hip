@@ -63,7 +63,13 @@ static void team_worker(Team* T, uint32_t r) {
         }
         (void)hipSetDevice(T->dev[r]);
         const int rc = fn(r);
-        if (rc) team_abort(T, "rank " + std::to_string(r) + ": " + T->rk[r]->err);
+        if (rc) {
+            team_abort(T, "rank " + std::to_string(r) + ": " + T->rk[r]->err);
+            // RCCL: this rank's collectives will never be matched; its
+            // communicators go now (the others abort theirs when they see the
+            // team aborted, sync_sharded), not after FRI_RCCL_TIMEOUT_S
+            if (T->kind == FRI_TRANSPORT_RCCL) rccl_abort(T->rk[r]);
+        }
         std::lock_guard<std::mutex> g(T->jm);
         T->rc[r] = rc;
         if (--T->left == 0) T->dcv.notify_all();
@@ -88,11 +94,16 @@ int fri::team_run(fri_ctx* root, const std::function<int(uint32_t)>& fn) {
     }
     T->jcv.notify_all();
     const int rc0 = fn(0);
-    if (rc0) team_abort(T, "rank 0: " + root->err);
+    if (rc0) {
+        team_abort(T, "rank 0: " + root->err);
+        if (T->kind == FRI_TRANSPORT_RCCL) rccl_abort(root);
+    }
     {
         std::unique_lock<std::mutex> lk(T->jm);
         T->dcv.wait(lk, [&] { return T->left == 0; });
     }
+    // fri_debug_team_inject_failure applies to this call only, fired or not
+    for (fri_ctx* c : T->rk) c->tp.fail_at = -1;
     int rc = rc0;
     for (uint32_t r = 1; r < T->G && !rc; r++) rc = T->rc[r];
     if (rc) {
@@ -113,6 +124,44 @@ int fri::team_run(fri_ctx* root, const std::function<int(uint32_t)>& fn) {
     return rc;
 }
 
+// Peer access is a per-process property of a device pair, shared by every
+// team of the process: reference-counted, enabled by the first team that
+// needs it and disabled when the last one is gone (never disabled when it was
+// enabled outside the library).
+struct PeerRef { int refs = 0; bool ours = false; };
+static std::mutex g_peer_m;
+static std::map<std::pair<int, int>, PeerRef> g_peer;
+
+static bool peer_acquire(int a, int b) {
+    std::lock_guard<std::mutex> g(g_peer_m);
+    PeerRef& pr = g_peer[{a, b}];
+    if (pr.refs == 0) {
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) return false;
+        (void)hipSetDevice(a);
+        const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        (void)hipGetLastError();
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return false;
+        pr.ours = e == hipSuccess;
+    }
+    pr.refs++;
+    return true;
+}
+
+static void peer_release(int a, int b) {
+    std::lock_guard<std::mutex> g(g_peer_m);
+    auto it = g_peer.find({a, b});
+    if (it == g_peer.end() || it->second.refs == 0) return;
+    if (--it->second.refs == 0) {
+        if (it->second.ours) {
+            (void)hipSetDevice(a);
+            (void)hipDeviceDisablePeerAccess(b);
+            (void)hipGetLastError();
+        }
+        g_peer.erase(it);
+    }
+}
+
 static void team_free(Team* T) {
     {
         std::lock_guard<std::mutex> g(T->jm);
@@ -125,6 +174,7 @@ static void team_free(Team* T) {
         if (r < T->ev_ready.size() && T->ev_ready[r]) { (void)hipSetDevice(T->dev[r]); hipEventDestroy(T->ev_ready[r]); }
         if (r < T->ev_done.size() && T->ev_done[r]) { (void)hipSetDevice(T->dev[r]); hipEventDestroy(T->ev_done[r]); }
     }
+    for (const auto& ab : T->peer_pairs) peer_release(ab.first, ab.second);
     delete T;
 }
 
@@ -157,9 +207,19 @@ extern "C" int fri_ctx_create_multi(const int* devices, uint32_t n, uint32_t log
     T->ev_done.assign(n, nullptr);
     int rc = FRI_OK;
     auto undo = [&](int code) {
+        // (communicators a later step's failure leaves behind are destroyed,
+        // not dropped: Transport() alone would leak them)
+        for (uint32_t r = 0; r < n; r++) {
+            fri_ctx* c = T->rk[r];
+            if (!c) continue;
+            (void)hipSetDevice(c->device);
+            if (c->tp.xcomm) ncclCommDestroy(c->tp.xcomm);
+            if (c->tp.comm) ncclCommDestroy(c->tp.comm);
+            c->tp = Transport();
+        }
         for (uint32_t r = 1; r < n; r++)
-            if (T->rk[r]) { T->rk[r]->tp = Transport(); fri_ctx_destroy(T->rk[r]); }
-        if (T->rk[0]) { T->rk[0]->tp = Transport(); T->rk[0]->team_root = nullptr; fri_ctx_destroy(T->rk[0]); }
+            if (T->rk[r]) fri_ctx_destroy(T->rk[r]);
+        if (T->rk[0]) { T->rk[0]->team_root = nullptr; fri_ctx_destroy(T->rk[0]); }
         team_free(T);
         return code;
     };
@@ -173,24 +233,28 @@ extern "C" int fri_ctx_create_multi(const int* devices, uint32_t n, uint32_t log
     }
     // peer access between distinct devices: the pull kernel reads the other
     // ranks' buffers over xGMI; without it, per-source hipMemcpyPeerAsync
+    // (fri_transport.hip peer_op; fri_debug_team_force_copy forces that path)
     for (uint32_t a = 0; a < n; a++)
         for (uint32_t b = 0; b < n; b++) {
             if (dev[a] == dev[b]) continue;
-            int can = 0;
-            if (hipDeviceCanAccessPeer(&can, dev[a], dev[b]) != hipSuccess || !can) { T->kernel_pull = false; continue; }
-            (void)hipSetDevice(dev[a]);
-            const hipError_t e = hipDeviceEnablePeerAccess(dev[b], 0);
-            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) T->kernel_pull = false;
-            (void)hipGetLastError();
+            if (std::find(T->peer_pairs.begin(), T->peer_pairs.end(), std::make_pair(dev[a], dev[b])) !=
+                T->peer_pairs.end())
+                continue;                        // (a device pair repeated by repeated ordinals)
+            if (peer_acquire(dev[a], dev[b])) T->peer_pairs.emplace_back(dev[a], dev[b]);
+            else T->can_pull = false;
         }
-    // transport: RCCL (one communicator per rank for the main stream, one for
-    // the exchange stream) when asked or when automatic and it initialises;
-    // ranks sharing a device can only use the peer transport
+    T->kernel_pull = T->can_pull;
+    // transport: the peer transport unless RCCL is asked for (FRI_TRANSPORT_NONE
+    // means peer: it is what the tests run; the in-process RCCL team has not
+    // yet run on distinct devices).  RCCL: one communicator per
+    // rank for the main stream, one for the exchange stream; ranks sharing a
+    // device cannot use it.
     bool distinct = true;
     for (uint32_t a = 0; a < n; a++)
         for (uint32_t b = a + 1; b < n; b++) distinct = distinct && dev[a] != dev[b];
     T->kind = FRI_TRANSPORT_PEER;
-    if (transport != FRI_TRANSPORT_PEER && distinct) {
+    if (transport == FRI_TRANSPORT_RCCL) {
+        if (!distinct) return undo(FRI_EINVAL);  // ranks share a device: RCCL cannot run them
         std::vector<ncclComm_t> c(n, nullptr), x(n, nullptr);
         ncclResult_t nr = ncclCommInitAll(c.data(), (int)n, dev.data());
         if (nr == ncclSuccess) {
@@ -198,15 +262,12 @@ extern "C" int fri_ctx_create_multi(const int* devices, uint32_t n, uint32_t log
             if (nr != ncclSuccess)
                 for (auto cm : c) ncclCommDestroy(cm);
         }
-        if (nr == ncclSuccess) {
-            T->kind = FRI_TRANSPORT_RCCL;
-            for (uint32_t r = 0; r < n; r++) { T->rk[r]->tp.comm = c[r]; T->rk[r]->tp.xcomm = x[r]; }
-        } else if (transport == FRI_TRANSPORT_RCCL) {
+        if (nr != ncclSuccess) {
             T->rk[0]->err = std::string("ncclCommInitAll: ") + ncclGetErrorString(nr);
             return undo(FRI_ERCCL);
         }
-    } else if (transport == FRI_TRANSPORT_RCCL) {
-        return undo(FRI_EINVAL);                 // ranks share a device: RCCL cannot run them
+        T->kind = FRI_TRANSPORT_RCCL;
+        for (uint32_t r = 0; r < n; r++) { T->rk[r]->tp.comm = c[r]; T->rk[r]->tp.xcomm = x[r]; }
     }
     for (uint32_t r = 0; r < n; r++) {
         Transport& tp = T->rk[r]->tp;
@@ -226,12 +287,67 @@ extern "C" int fri_ctx_create_multi(const int* devices, uint32_t n, uint32_t log
     return FRI_OK;
 }
 
+// The devices a caller that names none gets (fri_ctx_create_default):
+// FRI_DEVICES, else the largest power-of-two prefix of the visible devices.
+static int default_devices(std::vector<int>& dev, int& transport) {
+    dev.clear();
+    transport = FRI_TRANSPORT_PEER;
+    if (const char* t = getenv("FRI_TRANSPORT")) {
+        const std::string ts(t);
+        if (ts == "rccl") transport = FRI_TRANSPORT_RCCL;
+        else if (!ts.empty() && ts != "peer") return FRI_EINVAL;
+    }
+    const char* e = getenv("FRI_DEVICES");
+    if (e && *e) {
+        const std::string v(e);
+        size_t i = 0;
+        while (i <= v.size()) {
+            const size_t j = std::min(v.find(',', i), v.size());
+            const std::string tok = v.substr(i, j - i);
+            if (tok.empty() || tok.size() > 4 || tok.find_first_not_of("0123456789") != std::string::npos)
+                return FRI_EINVAL;
+            dev.push_back(atoi(tok.c_str()));
+            i = j + 1;
+        }
+        const size_t n = dev.size();
+        if (n == 0 || n > 64 || (n & (n - 1))) return FRI_EINVAL;
+        return FRI_OK;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return FRI_ENODEV;
+    int k = 1;
+    while (k * 2 <= std::min(ndev, 64)) k *= 2;
+    for (int r = 0; r < k; r++) dev.push_back(r);
+    return FRI_OK;
+}
+
+extern "C" int fri_ctx_create_default(uint32_t log_n_max, fri_ctx** out, uint32_t* n_ranks) {
+    if (!out) return FRI_EINVAL;
+    *out = nullptr;
+    std::vector<int> dev;
+    int transport = FRI_TRANSPORT_PEER;
+    const int rc = default_devices(dev, transport);
+    if (rc) return rc;
+    if (n_ranks) *n_ranks = (uint32_t)dev.size();
+    if (dev.size() == 1) return fri_ctx_create(dev[0], log_n_max, out);
+    return fri_ctx_create_multi(dev.data(), (uint32_t)dev.size(), log_n_max, transport, out);
+}
+
 extern "C" int fri_debug_team_inject_failure(fri_ctx* ctx, uint32_t rank, int64_t op_index) {
     if (!ctx) return FRI_EINVAL;
     if (!ctx->team_root || ctx->team_root->kind != FRI_TRANSPORT_PEER)
         return fail(ctx, FRI_EINVAL, "not a multi-GPU context on the peer transport");
     if (rank >= ctx->team_root->G) return fail(ctx, FRI_EINVAL, "rank out of range");
     ctx->team_root->rk[rank]->tp.fail_at = op_index;
+    return FRI_OK;
+}
+
+extern "C" int fri_debug_team_force_copy(fri_ctx* ctx, int enable) {
+    if (!ctx) return FRI_EINVAL;
+    if (!ctx->team_root || ctx->team_root->kind != FRI_TRANSPORT_PEER)
+        return fail(ctx, FRI_EINVAL, "not a multi-GPU context on the peer transport");
+    Team* T = ctx->team_root;
+    T->kernel_pull = T->can_pull && !enable;
     return FRI_OK;
 }
 
@@ -282,25 +398,43 @@ int fri::team_commit(fri_ctx* ctx, const uint32_t* host_coeffs, const uint32_t* 
     if (!out) return fail(ctx, FRI_EINVAL, "null argument");
     if (!team_shards(T, log_n))
         return run_commit(ctx, host_coeffs, dev_coeffs, d, log_n, offset, chan_in, flags, forced_betas, out);
-    // FRI_FLAG_RANK_INPUTS: each rank reads its own input buffer (resident
-    // since the last team commit that staged these coefficients)
+    // FRI_FLAG_RANK_INPUTS: ranks 1..G-1 commit the copy of rank 0's input
+    // buffer their plan staged at an earlier team commit instead of copying
+    // it again over xGMI.  Trusted only as far as it is checked: every rank
+    // first hashes the input it would commit (rank 0 the caller's buffer,
+    // the others their resident copy; k_checksum), and a rank whose copy
+    // differs (the caller rewrote the buffer since it was staged) makes the
+    // call return FRI_ESTATE on every rank before anything is committed.
     std::vector<const uint32_t*> din(T->G, dev_coeffs);
-    if (flags & FRI_FLAG_RANK_INPUTS) {
-        uint32_t logG = T->logG;
-        for (uint32_t r = 0; r < T->G; r++) {
+    const bool rank_inputs = (flags & FRI_FLAG_RANK_INPUTS) != 0;
+    if (rank_inputs) {
+        if (!d || !ctx->user_in || dev_coeffs != ctx->user_in || d > ctx->user_cap)
+            return fail(ctx, FRI_ESTATE, "FRI_FLAG_RANK_INPUTS: pass fri_ctx_input_buffer() (rank 0's input buffer)");
+        for (uint32_t r = 1; r < T->G; r++) {
             const fri_ctx* c = T->rk[r];
             const Plan& p = c->cur_lane == 0 ? c->plan : c->lanes[0].plan;
-            if (!p.valid || !p.sharded || p.d != d || p.log_n != log_n || p.offset != offset || p.G != T->G ||
-                (r == 0 && dev_coeffs != p.d_in) || log_n < logG)
-                return fail(ctx, FRI_ESTATE, "FRI_FLAG_RANK_INPUTS: commit these coefficients once without it, "
-                                             "and pass fri_ctx_input_buffer()");
+            if (!p.valid || !p.sharded || p.d != d || p.log_n != log_n || p.offset != offset || p.G != T->G)
+                return fail(ctx, FRI_ESTATE, "FRI_FLAG_RANK_INPUTS: no staged input of this shape on rank " +
+                                                 std::to_string(r) + ": commit these coefficients once without it");
             din[r] = p.d_in;
         }
     }
     const uint32_t fl = flags & ~FRI_FLAG_RANK_INPUTS;
     std::vector<fri_commit_result> res(T->G);
+    std::vector<uint64_t> sums(T->G, 0);
     int rc = team_run(ctx, [&](uint32_t r) {
-        return run_commit_sharded(T->rk[r], host_coeffs, din[r], d, log_n, offset, chan_in, fl, forced_betas, &res[r]);
+        fri_ctx* c = T->rk[r];
+        if (rank_inputs) {
+            int rs = input_checksum(c, din[r], d, &sums[r]);
+            if (rs) return rs;
+            if (!team_barrier(T)) return fail(c, FRI_ERCCL, "another rank failed (" + T->why + ")");
+            for (uint32_t q = 1; q < T->G; q++)
+                if (sums[q] != sums[0])
+                    return fail(c, FRI_ESTATE, "FRI_FLAG_RANK_INPUTS: rank " + std::to_string(q) +
+                                                   "'s staged input differs from rank 0's input buffer (rewritten "
+                                                   "since it was staged): commit without the flag to stage it");
+        }
+        return run_commit_sharded(c, host_coeffs, din[r], d, log_n, offset, chan_in, fl, forced_betas, &res[r]);
     });
     if (rc) return rc;
     // the redundant tops give every rank the whole transcript: they must agree

@@ -62,12 +62,23 @@ int fri::sync_sharded(fri_ctx* ctx, hipStream_t s) {
     // spin (yielding) for the first 200 us, which covers a commit's short
     // syncs at full responsiveness, then poll every 50 us so that a rank
     // waiting on its peers does not hold a host core at 100%
+    // A rank of an RCCL team whose peer failed stops waiting at once: that
+    // rank aborted its communicators (team_run), so the collectives it left
+    // behind are never matched; this rank aborts its own as well.
+    Team* T = ctx->tp.team;
+    auto team_failed = [T]() {
+        if (!T) return false;
+        std::lock_guard<std::mutex> g(T->bm);
+        return T->aborted;
+    };
+    bool peer_failed = false;
     for (;;) {
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) return FRI_OK;
         if (e != hipErrorNotReady) FRI_HIP(ctx, e);
         const double el = seconds_since(t0);
         if (el > lim) break;
+        if ((peer_failed = team_failed())) break;
         if (el < 2e-4) std::this_thread::yield();
         else std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
@@ -80,8 +91,9 @@ int fri::sync_sharded(fri_ctx* ctx, hipStream_t s) {
     while (!(drained = hipStreamQuery(s) != hipErrorNotReady) && seconds_since(t1) < lim)
         std::this_thread::sleep_for(std::chrono::microseconds(200));
     if (!drained) ctx->stuck = true;      // fri_ctx_destroy must not wait on it unboundedly
-    return fail(ctx, FRI_ERCCL, "sharded commit: no progress in " + std::to_string((int)lim) +
-                                    " s (RCCL communicators aborted" +
+    const std::string why = peer_failed ? std::string("another rank of the team failed")
+                                        : "no progress in " + std::to_string((int)lim) + " s";
+    return fail(ctx, FRI_ERCCL, "sharded commit: " + why + " (RCCL communicators aborted" +
                                     (drained ? ")" : "; stream still busy: destroy the context)"));
 }
 static const char* op_name(uint32_t op) {

@@ -194,11 +194,21 @@ Gpu::Gpu(int device, uint32_t log_n_max) : log_n_max_(log_n_max) {
     }
 }
 
-Gpu::Gpu(const std::vector<int>& devices, uint32_t log_n_max, int transport) : log_n_max_(log_n_max) {
+Gpu::Gpu(const std::vector<int>& devices, uint32_t log_n_max, int transport)
+    : log_n_max_(log_n_max), n_ranks_(static_cast<uint32_t>(devices.size())) {
     int rc = fri_ctx_create_multi(devices.data(), static_cast<uint32_t>(devices.size()), log_n_max, transport, &ctx_);
     if (rc != FRI_OK) {
         ctx_ = nullptr;
         throw Panic("fri_ctx_create_multi failed (code " + std::to_string(rc) + ")");
+    }
+}
+
+Gpu::Gpu(Default, uint32_t log_n_max) : log_n_max_(log_n_max) {
+    int rc = fri_ctx_create_default(log_n_max, &ctx_, &n_ranks_);
+    if (rc != FRI_OK) {
+        ctx_ = nullptr;
+        throw Panic("fri_ctx_create_default failed (code " + std::to_string(rc) +
+                    (rc == FRI_EINVAL ? ": malformed FRI_DEVICES / FRI_TRANSPORT)" : ")"));
     }
 }
 
@@ -213,7 +223,7 @@ void Gpu::check(int rc, const char* what) const {
 std::shared_ptr<Gpu> Gpu::thread_default(uint32_t log_n) {
     static thread_local std::shared_ptr<Gpu> g;
     const uint32_t want = log_n < 12 ? 12 : log_n;
-    if (!g || g->log_n_max() < want) g = std::make_shared<Gpu>(0, want);
+    if (!g || g->log_n_max() < want) g = std::make_shared<Gpu>(Gpu::Default{}, want);
     return g;
 }
 
@@ -432,20 +442,31 @@ FRIProof fri_commit(const Poly& poly, const Coset& coset, FriChannel& channel) {
 }
 
 // ------------------------------------------------------------------ decommit
-void decommit_fri_layers(size_t index, const FRIProof& proof, FriChannel& channel) {
-    proof.require_resident();
-    const size_t L = proof.n_layers();
+namespace {
+// One query (decommit_fri_layers, fri_commit.rs:137-163) through the gather
+// kernel on the commit resident on `gpu`: per layer send value, path,
+// sibling value, sibling path (a 1-element layer sends its value first).
+// `layers` (optional): the caller's FRIProof.fri_layers, checked against the
+// device's openings.
+void decommit_query(const Gpu& gpu, uint32_t log_n, size_t n_layers, uint64_t index, FriChannel& channel,
+                    const std::vector<std::vector<FE>>* layers) {
     size_t path_bytes = 0;
-    for (size_t k = 0; k < L; k++) path_bytes += 2 * 32 * (proof.log_n - k);
-    std::vector<uint32_t> values(2 * L);
+    for (size_t k = 0; k < n_layers; k++) path_bytes += 2 * 32 * (log_n - k);
+    std::vector<uint32_t> values(2 * n_layers);
     std::vector<uint8_t> paths(path_bytes ? path_bytes : 1);
     size_t got = 0;
-    proof.gpu_->check(fri_decommit_query(proof.gpu_->ctx(), index, values.data(), values.size(), paths.data(),
-                                         paths.size(), &got),
-                      "fri_decommit_query");
+    gpu.check(fri_decommit_query(gpu.ctx(), index, values.data(), values.size(), paths.data(), paths.size(), &got),
+              "fri_decommit_query");
     size_t off = 0;
-    for (size_t k = 0; k < L; k++) {
-        const size_t depth = proof.log_n - k, pb = 32 * depth;
+    for (size_t k = 0; k < n_layers; k++) {
+        const size_t depth = log_n - k, pb = 32 * depth, m = size_t{1} << depth;
+        if (layers) {
+            const std::vector<FE>& lk = (*layers)[k];
+            const size_t i = index % m, sib = (i + m / 2) % m;
+            if (lk.size() != m || lk[i].value() != values[2 * k] || lk[sib].value() != values[2 * k + 1])
+                throw Panic("fri_layers do not belong to the commit of these fri_merkles (layer " + std::to_string(k) +
+                            ")");
+        }
         std::vector<uint8_t> path(paths.begin() + off, paths.begin() + off + pb);
         std::vector<uint8_t> spath(paths.begin() + off + pb, paths.begin() + off + 2 * pb);
         off += 2 * pb;
@@ -457,11 +478,41 @@ void decommit_fri_layers(size_t index, const FRIProof& proof, FriChannel& channe
         channel.send(spath);
     }
 }
+}  // namespace
+
+void decommit_fri_layers(size_t index, const FRIProof& proof, FriChannel& channel) {
+    proof.require_resident();
+    decommit_query(*proof.gpu_, proof.log_n, proof.n_layers(), index, channel, nullptr);
+}
 
 void decommit_fri(size_t num_queries, size_t max_index, const FRIProof& proof, FriChannel& channel) {
     for (size_t q = 0; q < num_queries; q++) {
         const uint64_t idx = channel.receive_random_int(0, max_index, true);
         decommit_fri_layers(idx, proof, channel);
+    }
+}
+
+void decommit_fri(size_t num_queries, size_t max_index, const std::vector<std::vector<FE>>& fri_layers,
+                  const std::vector<MerkleTree>& fri_merkles, FriChannel& channel) {
+    if (fri_merkles.empty()) throw Panic("decommit_fri: no FRI layers");
+    if (fri_layers.size() != fri_merkles.size()) throw Panic("decommit_fri: one Merkle tree per FRI layer");
+    const MerkleTree& t0 = fri_merkles[0];
+    if (!t0.gpu_) throw Panic("decommit_fri: the trees of an FRIProof are device-backed; a standalone tree keeps only its root");
+    for (size_t k = 0; k < fri_merkles.size(); k++) {
+        const MerkleTree& t = fri_merkles[k];
+        if (t.gpu_ != t0.gpu_ || t.gen_ != t0.gen_ || t.layer_ != k)
+            throw Panic("decommit_fri: the trees are not the layers of one commit");
+    }
+    const Gpu& gpu = *t0.gpu_;
+    if (gpu.generation() != t0.gen_) throw Panic("FRIProof layers were replaced by a later commit on the same Gpu");
+    uint64_t g = 0;
+    uint32_t log_n = 0, n_layers = 0;
+    gpu.check(fri_commit_info(gpu.ctx(), &g, &log_n, &n_layers), "fri_commit_info");
+    if (n_layers != fri_merkles.size() || fri_layers[0].size() != (size_t{1} << log_n))
+        throw Panic("decommit_fri: the resident commit is not the one these trees belong to");
+    for (size_t q = 0; q < num_queries; q++) {
+        const uint64_t idx = channel.receive_random_int(0, max_index, true);
+        decommit_query(gpu, log_n, n_layers, idx, channel, &fri_layers);
     }
 }
 

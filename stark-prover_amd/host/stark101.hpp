@@ -256,28 +256,38 @@ class Gpu {
   public:
     Gpu(int device, uint32_t log_n_max);
     // A team over several GPUs driven from this thread (fri_ctx_create_multi;
-    // a device may repeat; transport FRI_TRANSPORT_NONE = RCCL if it
-    // initialises, else peer).  Every call below takes it unchanged: a
-    // codeword >= 2^20 is committed coset-sharded over the devices by ONE
-    // fri_commit, and the proof's layers and trees serve as on one GPU.
+    // a device may repeat; transport FRI_TRANSPORT_NONE = the peer
+    // transport, FRI_TRANSPORT_RCCL opt-in).  Every call below takes it
+    // unchanged: a codeword >= 2^20 is committed coset-sharded over the
+    // devices by ONE fri_commit, and the proof's layers and trees serve as on
+    // one GPU.
     Gpu(const std::vector<int>& devices, uint32_t log_n_max, int transport = FRI_TRANSPORT_NONE);
+    // The default devices (fri_ctx_create_default): FRI_DEVICES, else every
+    // visible GPU (the largest power-of-two count); one device is an
+    // ordinary context, several a team.
+    struct Default {};
+    Gpu(Default, uint32_t log_n_max);
     ~Gpu();
     Gpu(const Gpu&) = delete;
     Gpu& operator=(const Gpu&) = delete;
     fri_ctx* ctx() const { return ctx_; }
     uint32_t log_n_max() const { return log_n_max_; }
     uint64_t generation() const { return gen_; }
+    uint32_t n_ranks() const { return n_ranks_; }
     uint64_t bump() { return ++gen_; }
     // Throws Panic("<what>: <fri_last_error>") when rc != FRI_OK.
     void check(int rc, const char* what) const;
-    // Per-thread context on device 0 holding at least 2^log_n (grown by
-    // replacing it; FRIProofs keep the old one alive).
+    // The context behind the reference-signature calls (fri_commit(poly,
+    // domain, channel), MerkleTree, interpolate, ...): per thread (a context
+    // is not re-entrant), over the default devices (Gpu(Default, ...)), at
+    // least 2^log_n (grown by replacing it; FRIProofs keep the old one alive).
     static std::shared_ptr<Gpu> thread_default(uint32_t log_n);
 
   private:
     fri_ctx* ctx_ = nullptr;
     uint32_t log_n_max_ = 0;
     uint64_t gen_ = 0;
+    uint32_t n_ranks_ = 1;
 };
 
 class FRIProof;
@@ -295,6 +305,8 @@ class MerkleTree {
 
   private:
     friend class FRIProof;
+    friend void decommit_fri(size_t, size_t, const std::vector<std::vector<FE>>&, const std::vector<MerkleTree>&,
+                             FriChannel&);
     friend FRIProof fri_commit_coset(const Poly&, uint32_t, FE, FriChannel&, const std::shared_ptr<Gpu>&);
     friend std::vector<FRIProof> fri_commit_pipelined(const std::vector<Poly>&, uint32_t, FE, std::vector<FriChannel>&,
                                                       const std::shared_ptr<Gpu>&);
@@ -358,6 +370,14 @@ std::vector<FRIProof> fri_commit_pipelined(const std::vector<Poly>& polys, uint3
 // fri_commit.rs:137-179 over the device-resident layers and trees.
 void decommit_fri_layers(size_t index, const FRIProof& proof, FriChannel& channel);
 void decommit_fri(size_t num_queries, size_t max_index, const FRIProof& proof, FriChannel& channel);
+// The reference's own signature, decommit_fri(num_queries, max_index,
+// &fri_layers, &fri_merkles, &mut channel) (fri_commit.rs:168-174): the
+// commit is found through the device-backed trees (their Gpu and
+// generation; a stale or standalone tree panics), the openings are gathered
+// on the device and checked against `fri_layers` (a mismatch panics: the
+// layers belong to another commit).
+void decommit_fri(size_t num_queries, size_t max_index, const std::vector<std::vector<FE>>& fri_layers,
+                  const std::vector<MerkleTree>& fri_merkles, FriChannel& channel);
 
 // Checks a transcript (the messages fri_commit then decommit_fri appended to
 // Channel::proof).  The reference's fri_verify.rs:12-177 is a sketch (it

@@ -119,6 +119,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "fri_commit_async": (i32, [vp, pu32, sz, u32, u32, ctypes.POINTER(ChannelState), u32, pu32,
                                    ctypes.POINTER(ctypes.c_uint64)]),
         "fri_ctx_input_buffer": (i32, [vp, sz, ctypes.POINTER(vp)]),
+        "fri_ctx_input_upload": (i32, [vp, pu32, sz]),
+        "fri_ctx_create_default": (i32, [u32, ctypes.POINTER(vp), ctypes.POINTER(u32)]),
+        "fri_debug_team_force_copy": (i32, [vp, i32]),
         "fri_commit_info": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "fri_layer_copy": (i32, [vp, u32, pu32, sz]),
         "fri_tree_level_copy": (i32, [vp, u32, u32, ctypes.c_char_p, sz]),
@@ -205,8 +208,8 @@ class Context:
         """fri_ctx_create_multi: ONE context over len(devices) GPUs (ranks;
         a device may repeat), driven from this thread.  commit / commit_device
         of a codeword >= 2^20 run coset-sharded over the ranks in one call;
-        every read-back serves the whole commit.  transport: "auto" (RCCL if
-        it initialises, else peer), "rccl" or "peer"."""
+        every read-back serves the whole commit.  transport: "auto" (the
+        peer transport), "peer" or "rccl" (opt-in, distinct devices only)."""
         lib = load_library()
         kinds = {"auto": 0, "rccl": 1, "peer": 4}
         if transport not in kinds:
@@ -220,6 +223,43 @@ class Context:
         c.n_ranks = len(devices)
         c.devices = [int(x) for x in devices]
         return c
+
+    @classmethod
+    def default(cls, log_n_max: int) -> "Context":
+        """fri_ctx_create_default: the devices named by FRI_DEVICES (e.g.
+        "0,0,0,0"), else every visible GPU (largest power-of-two count); one
+        device is an ordinary context, several a team (peer transport, or
+        FRI_TRANSPORT=rccl).  What the reference-shaped functions below use
+        when no ctx is passed."""
+        lib = load_library()
+        h = ctypes.c_void_p()
+        n = ctypes.c_uint32()
+        rc = lib.fri_ctx_create_default(log_n_max, ctypes.byref(h), ctypes.byref(n))
+        if rc != FRI_OK:
+            raise FriError(rc, f"fri_ctx_create_default({log_n_max}) failed (FRI_DEVICES="
+                               f"{os.environ.get('FRI_DEVICES', '')!r}; no gfx950 device?)")
+        c = cls(0, log_n_max, _handle=h)
+        c.n_ranks = n.value
+        return c
+
+    def input_buffer(self, d: int) -> int:
+        """Device pointer of the context's input buffer (fri_ctx_input_buffer):
+        the caller's; no commit writes it, commits from it read it in place."""
+        p = ctypes.c_void_p()
+        self._check(self.lib.fri_ctx_input_buffer(self.h, d, ctypes.byref(p)))
+        return p.value
+
+    def input_upload(self, coeffs) -> int:
+        """Fill the input buffer with host coefficients (fri_ctx_input_upload;
+        waits for the pending commits reading it) and return its pointer."""
+        c = _u32(coeffs)
+        self._check(self.lib.fri_ctx_input_upload(self.h, _ptr(c), c.size))
+        return self.input_buffer(c.size)
+
+    def force_copy(self, enable: bool = True):
+        """Test hook (fri_debug_team_force_copy): a team's collectives copy with
+        hipMemcpyPeerAsync per source instead of the pull kernel."""
+        self._check(self.lib.fri_debug_team_force_copy(self.h, 1 if enable else 0))
 
     def team_rank(self, rank: int) -> "Context":
         """A non-owning view of rank ``rank``'s context (fri_debug_team_rank),
@@ -741,14 +781,38 @@ class Channel:
 
 
 class MerkleTree:
-    """src/merkle/mod.rs:5-27 — SHA-256 tree over u64-BE leaves (GPU-built)."""
+    """src/merkle/mod.rs:5-27 — SHA-256 tree over u64-BE leaves (GPU-built).
+    A standalone tree keeps its root; the trees of an FRIProof
+    (``FRIProof.fri_merkles``) are the device-resident ones of that commit
+    and also serve authentication paths."""
 
     def __init__(self, values: Sequence[int], ctx: Optional[Context] = None):
         self._ctx = ctx or _default_ctx(max(1, (len(values) - 1).bit_length()))
         self._root = self._ctx.merkle_root(values)
+        self._generation = None
+        self._layer = None
+        self._log_n = None
+        self._sharded = False
+
+    @classmethod
+    def _on_device(cls, ctx: Context, generation: int, layer: int, log_n: int, root: bytes,
+                   sharded: bool = False) -> "MerkleTree":
+        t = cls.__new__(cls)
+        t._ctx, t._root, t._generation, t._layer, t._log_n = ctx, root, generation, layer, log_n
+        t._sharded = sharded
+        return t
 
     def root(self) -> str:
         return self._root.hex()
+
+    def get_authentication_path(self, idx: int) -> bytes:
+        """rs_merkle single-leaf proof of leaf idx (sibling digests leaf ->
+        root) from the device-resident tree (fri_auth_path)."""
+        if self._generation is None:
+            raise FriError(FRI_ESTATE, "a standalone tree keeps only its root")
+        self._ctx._resident(self._log_n, self._generation)
+        _, path = self._ctx.auth_path(self._layer, idx, self._log_n)
+        return b"".join(path)
 
 
 @dataclass
@@ -778,6 +842,12 @@ class FRIProof:
         return self.roots[k].hex()
 
     @property
+    def fri_merkles(self) -> List[MerkleTree]:
+        """FRIProof.fri_merkles (fri_commit.rs:9-13): the commit's trees, device-backed."""
+        return [MerkleTree._on_device(self.ctx, self.generation, k, self.log_n, r, self.sharded)
+                for k, r in enumerate(self.roots)]
+
+    @property
     def final_poly(self) -> List[int]:
         return [] if self.final_degree == -1 else [self.final_value]
 
@@ -786,8 +856,12 @@ def decommit_fri_layers(index: int, proof: "FRIProof", channel: Channel) -> None
     """src/fri/fri_commit.rs:137-163 over the device-resident layers/trees:
     per layer send value, path, sibling value, sibling path (a 1-element
     layer first sends its value, as the reference does)."""
-    for val, sval, path, spath in proof.ctx.decommit_query(index, proof.n_layers, proof.log_n, proof.generation,
-                                                           proof.sharded):
+    _send_openings(proof.ctx.decommit_query(index, proof.n_layers, proof.log_n, proof.generation, proof.sharded),
+                   channel)
+
+
+def _send_openings(openings, channel: Channel) -> None:
+    for val, sval, path, spath in openings:
         # the gather reads layers of 2^(log_n-k) >= 2 elements; a 1-element
         # layer (blowup 1) has idx = sib = 0 and empty paths
         if not path and not spath:
@@ -798,12 +872,36 @@ def decommit_fri_layers(index: int, proof: "FRIProof", channel: Channel) -> None
         channel.send(spath)
 
 
-def decommit_fri(num_queries: int, max_index: int, proof: "FRIProof", channel: Channel) -> None:
+def decommit_fri(num_queries: int, max_index: int, proof, merkles_or_channel, channel: Optional[Channel] = None) -> None:
     """src/fri/fri_commit.rs:168-179: each index drawn with
-    receive_random_int(0, max_index, true) from the transcript so far."""
+    receive_random_int(0, max_index, true) from the transcript so far.
+    Two forms: decommit_fri(q, max, proof, channel), or the reference's own
+    decommit_fri(q, max, fri_layers, fri_merkles, channel) with the proof's
+    ``fri_layers`` and device-backed ``fri_merkles`` (the commit is found
+    through the trees; their generation must still be resident, and the
+    openings must equal ``fri_layers``)."""
+    if channel is None:
+        for _ in range(num_queries):
+            idx = merkles_or_channel.receive_random_int(0, max_index, True)
+            decommit_fri_layers(idx, proof, merkles_or_channel)
+        return
+    layers, merkles = proof, merkles_or_channel
+    if not merkles or len(layers) != len(merkles):
+        raise FriError(FRI_EINVAL, "one Merkle tree per FRI layer")
+    t0 = merkles[0]
+    if t0._generation is None or any(t._ctx is not t0._ctx or t._generation != t0._generation or t._layer != k
+                                     for k, t in enumerate(merkles)):
+        raise FriError(FRI_EINVAL, "fri_merkles are not the device-backed trees of one commit")
+    ctx, log_n = t0._ctx, t0._log_n
     for _ in range(num_queries):
         idx = channel.receive_random_int(0, max_index, True)
-        decommit_fri_layers(idx, proof, channel)
+        openings = ctx.decommit_query(idx, len(merkles), log_n, t0._generation, t0._sharded)
+        for k, (v, sv, _, _) in enumerate(openings):
+            m = 1 << (log_n - k)
+            i = idx % m
+            if len(layers[k]) != m or int(layers[k][i]) != v or int(layers[k][(i + m // 2) % m]) != sv:
+                raise FriError(FRI_ESTATE, f"fri_layers do not belong to the commit of these fri_merkles (layer {k})")
+        _send_openings(openings, channel)
 
 
 def _merkle_path_ok(value: int, index: int, path: bytes, depth: int, root: bytes) -> bool:
@@ -1039,11 +1137,14 @@ _CTX_CACHE = {}
 
 
 def _default_ctx(log_n: int) -> Context:
+    """The context of the reference-shaped calls without ``ctx``: over the
+    default devices (Context.default: FRI_DEVICES, else every visible GPU),
+    at least 2^log_n (2^12 minimum), one per size bound, kept."""
     key = max(log_n, 12)
     for k, c in _CTX_CACHE.items():
         if k >= key:
             return c
-    c = Context(0, key)
+    c = Context.default(key)
     _CTX_CACHE[key] = c
     return c
 

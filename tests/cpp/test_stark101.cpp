@@ -8,6 +8,7 @@
 //        inverse through libfri_amd.so against tests/golden (bit-exact).
 // Usage: test_stark101 [cpu|gpu|all]; exit status = number of failures.
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -588,8 +589,58 @@ TEST(gpu, prove_fibsq_matches_golden) {
     ASSERT_TRUE(!verify_fibsq(bad, sp.a_last, 16, 3, 3, sp.fri.n_layers()));
 }
 
+// ---------------------------------------------------------------------------
+// `test_stark101 refsig LOG_N OUT`: the reference's own signatures with no
+// context named anywhere -- fri_commit(poly, domain, &mut channel) and
+// decommit_fri(num_queries, max_index, &fri_layers, &fri_merkles,
+// &mut channel) (fri_commit.rs:72-76,168-174) -- on the default devices
+// (FRI_DEVICES; tests/test_cpp_host.py runs it with "0,0,0,0", a four-rank
+// team on one GPU).  Writes the rank count, every Channel::proof message and
+// the final state to OUT (one hex line each) for the test to compare with
+// the C oracle; then checks that a later commit makes the old proof's
+// decommitment panic and that layers of another commit are refused.
+static uint64_t splitmix64_at(uint64_t seed, uint64_t i) {       // fri_oracle.splitmix64_np, element i (0-based)
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static int refsig(uint32_t log_n, const char* out_path) {
+    const size_t n = size_t{1} << log_n, d = n >> 3;
+    std::vector<FE> cs(d);
+    for (size_t i = 0; i < d; i++) cs[i] = FE(splitmix64_at(42, i) % P);
+    FriChannel ch;
+    FRIProof proof = fri_commit(Poly(cs), Coset(FE(FRI_GENERATOR), omega(log_n), n).generate_coset_domain(), ch);
+    const auto layers = proof.fri_layers();
+    decommit_fri(2, n - 1, layers, proof.fri_merkles, ch);
+    FILE* f = std::fopen(out_path, "w");
+    if (!f) return 2;
+    std::fprintf(f, "ranks %u\n", Gpu::thread_default(log_n)->n_ranks());
+    std::fprintf(f, "state %s\n", ch.state.c_str());
+    for (const auto& m : ch.proof) std::fprintf(f, "msg %s\n", sha::hex(m.data(), m.size()).c_str());
+    std::fclose(f);
+    int fails = 0;
+    // the layers of another commit are refused (checked against the device's openings)
+    auto wrong = layers;
+    for (auto& v : wrong[1]) v = v + FE(1);
+    FriChannel c1 = ch;
+    bool refused = false;
+    try { decommit_fri(4, n - 1, wrong, proof.fri_merkles, c1); } catch (const Panic&) { refused = true; }
+    if (!refused) { std::printf("FAIL refsig: layers of another commit accepted\n"); fails++; }
+    // a later commit on the same (default) Gpu retires the proof
+    FriChannel ch2;
+    fri_commit(Poly(std::vector<FE>(cs.begin(), cs.begin() + d / 2)), Coset(FE(FRI_GENERATOR), omega(log_n), n), ch2);
+    bool stale = false;
+    FriChannel c2 = ch;
+    try { decommit_fri(1, n - 1, layers, proof.fri_merkles, c2); } catch (const Panic&) { stale = true; }
+    if (!stale) { std::printf("FAIL refsig: stale proof decommitted\n"); fails++; }
+    std::printf("refsig 2^%u: %zu messages, %d failures\n", log_n, ch.proof.size(), fails);
+    return fails;
+}
+
 int main(int argc, char** argv) {
     const std::string which = argc > 1 ? argv[1] : "cpu";
+    if (which == "refsig") return argc > 3 ? refsig(static_cast<uint32_t>(std::atoi(argv[2])), argv[3]) : 2;
     int fails = 0, ran = 0;
     for (auto& t : registry()) {
         if (which != "all" && which != t.group) continue;

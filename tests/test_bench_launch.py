@@ -74,3 +74,17 @@ def test_source_hash_covers_the_kernels():
     names = {os.path.basename(f) for f in files}
     assert {"fri_layer.hip", "fri_kernels.hip", "fri_commit.hip", "fri_host.hpp", "sha256_fast.hpp", "fri_amd.h", "Makefile"} <= names
     assert len(bench.source_hash()) == 64
+
+
+@pytest.mark.parametrize("team,world,ndev,ranks,want", [
+    (None, 1, 1, 1, (1, False)),                 # the default 1-GPU line
+    (None, 8, 8, 8, (8, False)),                 # torchrun x8 on an 8-GPU node
+    (None, 2, 1, 2, (1, True)),                  # 2 ranks on the 1-GPU box: a rehearsal
+    ([0, 1, 2, 3], 1, 8, 4, (4, False)),         # p2p team over 4 GPUs
+    ([0, 0], 1, 1, 2, (1, True)),                # p2p team, 2 ranks on one GPU
+])
+def test_devices_used_reports_distinct_gpus(team, world, ndev, ranks, want):
+    """n_gpus in the line is the number of distinct devices; ranks sharing a
+    device mark the run oversubscribed (such a run is not an
+    N-GPU scaling point)."""
+    assert bench.devices_used(team, world, ndev, ranks) == want

@@ -73,3 +73,34 @@ def test_cpp_host_mirror_gpu():
     assert "ok   gpu::fri_commit_and_decommit_match_golden" in out
     assert "ok   gpu::fri_commit_pipelined_matches_golden" in out
     assert "ok   gpu::prove_fibsq_matches_golden" in out
+
+
+@pytest.mark.gpu
+def test_cpp_reference_signatures_on_default_team(tmp_path, corc):
+    """The reference's own signatures, no context named anywhere:
+    fri_commit(poly, domain, &mut channel) and decommit_fri(num_queries,
+    max_index, &fri_layers, &fri_merkles, &mut channel)
+    (fri_commit.rs:72-76,168-174) through the C++ mirror, whose per-thread
+    default context is a team over FRI_DEVICES ("0,0,0,0": four ranks on the
+    one GPU of the box; on an 8-GPU node, unset, it would be all eight).  At
+    2^22 the commit is coset-sharded; the whole transcript -- every root, beta,
+    the final value and two queries' openings -- equals the C oracle's, a
+    later commit makes the old proof's decommitment panic, and layers of
+    another commit are refused (tests/cpp/test_stark101.cpp refsig)."""
+    import numpy as np
+
+    import fri_oracle as fo
+    import oracle_flat
+    _build()
+    out = tmp_path / "refsig.txt"
+    env = dict(os.environ, FRI_DEVICES="0,0,0,0")
+    p = subprocess.run([BIN, "refsig", "22", str(out)], capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    lines = out.read_text().split("\n")
+    assert lines[0] == "ranks 4", lines[0]
+    state = lines[1].split()[1]
+    msgs = [bytes.fromhex(ln.split()[1]) if len(ln.split()) > 1 else b"" for ln in lines[2:] if ln.startswith("msg")]
+    want_msgs, want_state = oracle_flat.transcript(corc, fo.splitmix64_np(42, (1 << 22) >> 3), 22, 2)
+    assert len(msgs) == len(want_msgs)
+    assert msgs == want_msgs
+    assert state == want_state

@@ -462,9 +462,8 @@ def test_noncanonical_input_rejected_on_device(ctx, oracle, oracle_commit, log_n
         ctx.commit(bad, log_n)
     assert e.value.code == fri_amd.FRI_EINVAL
     assert ctx.commit_info()[2] == 0                                    # no layers served
-    # the same input through fri_commit_device (the host call left it in the input buffer)
-    dptr = ctypes.c_void_p()
-    ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(dptr)))
+    # the same input through fri_commit_device, from the context's input buffer
+    dptr = ctypes.c_void_p(ctx.input_upload(bad))
     res = fri_amd.CommitResult()
     rc = ctx.lib.fri_commit_device(ctx.h, dptr, d, log_n, fri_amd.GENERATOR, None, 0, None, ctypes.byref(res))
     assert rc == fri_amd.FRI_EINVAL

@@ -344,17 +344,14 @@ def test_commit_lanes(pctx, oracle, oracle_commit, torch):
 def test_lanes_sync_commit_and_input_buffer(pctx, oracle, oracle_commit, torch):
     """A synchronous commit runs on lane 0 while a pipelined commit is still
     pending on lane 1; both transcripts are right and the read-backs then
-    serve the synchronous one.  The context's input buffer (lane 0's) stays
-    the same pointer across lanes, and a pipelined commit on another lane
-    reads it correctly."""
-    import fri_amd
+    serve the synchronous one.  The context's input buffer keeps its pointer,
+    holds what the caller uploaded whatever is committed in between, and
+    pipelined commits on every lane read it in place."""
     d = (1 << LOG_N) >> 3
     (s1, b1), (s2, b2) = _polys(oracle, torch, [1011, 1012])
     c3 = oracle.splitmix64_np(1013, d).astype(np.uint32)
     pctx.set_lanes(4)
-    pctx.commit(c3, LOG_N)
-    p0 = ctypes.c_void_p()
-    pctx._check(pctx.lib.fri_ctx_input_buffer(pctx.h, d, ctypes.byref(p0)))
+    p0 = pctx.input_upload(c3)                                       # the caller's buffer holds c3
     t1 = pctx.commit_device_async(b1.data_ptr(), d, LOG_N)          # lane 0
     t2 = pctx.commit_device_async(b2.data_ptr(), d, LOG_N)          # lane 1
     assert _transcript(pctx.commit_wait(t1)) == oracle_commit(LOG_N, s1)
@@ -364,70 +361,92 @@ def test_lanes_sync_commit_and_input_buffer(pctx, oracle, oracle_commit, torch):
     assert pctx.layer(2, LOG_N).size == 1 << (LOG_N - 2)
     val, _ = pctx.auth_path(0, 5, LOG_N)
     assert int(val) == int(pctx.lde(c3[:d], LOG_N)[5])               # the sync commit's layer 0
-    p1 = ctypes.c_void_p()
-    pctx._check(pctx.lib.fri_ctx_input_buffer(pctx.h, d, ctypes.byref(p1)))
-    assert p1.value == p0.value
-    ta = pctx.commit_device_async(b1.data_ptr(), d, LOG_N)          # lane 0 (stages b1 in the input buffer)
+    assert pctx.input_buffer(d) == p0
+    ta = pctx.commit_device_async(b1.data_ptr(), d, LOG_N)          # another pointer: staged privately
     pctx.commit_wait(ta)
-    pctx.commit(c3, LOG_N)                                           # the input buffer holds c3 again
-    ts = [pctx.commit_device_async(p0.value, d, LOG_N) for _ in range(3)]   # lanes 0, 1, 2 read it
+    pctx.commit(oracle.splitmix64_np(1014, d).astype(np.uint32), LOG_N)   # host input: staged privately
+    ts = [pctx.commit_device_async(p0, d, LOG_N) for _ in range(4)]       # lanes 0-3 read the buffer in place
     for t in ts:
         assert _transcript(pctx.commit_wait(t)) == oracle_commit(LOG_N, 1013)
 
 
-def test_input_buffer_read_in_call_order_across_lanes(oracle, oracle_commit, torch):
-    """Lane 0's input buffer (fri_ctx_input_buffer) handed to a pipelined
-    commit D on lane 1: D must commit what the buffer holds in call order.
-    Commits on lane 0 from other pointers stage their coefficients into that
-    buffer, so D's copy of it is made on lane 0's stream (commit_enqueue in
-    fri_lanes.hip): after the stagings of the commits enqueued before D, before
-    those of later ones.  Here lane 0 runs two commits that stage a polynomial
-    with a coefficient >= p (they stop after layer 0 with FRI_EINVAL) while
-    lane 1 runs a whole 2^24 commit B before D; then a synchronous commit
-    stages P2.  In call order D reads the rejected polynomial, so D fails with
-    FRI_EINVAL; a copy made on lane 1's own stream would read P2 instead and
-    commit it.  A second round checks a valid staging: D then commits the
-    polynomial staged just before it."""
+@pytest.mark.parametrize("log_n,lanes", [(LOG_N, 3), (20, 3), (LOG_N, 1)])
+def test_input_buffer_independent_of_lane_deal(oracle, oracle_commit, torch, log_n, lanes):
+    """The input buffer belongs to the caller (fri_commit.rs:72-76: the
+    caller owns poly): with four commits pending, commits from it are mixed
+    with commits from other device buffers and from host coefficients (which
+    the library stages privately), dealt to whichever lane; every commit from
+    the buffer commits what the caller last uploaded there, and an upload
+    (fri_ctx_input_upload) waits for the pending commits that still read the
+    old contents.  Every transcript equals the C oracle's."""
     import fri_amd
-    L = 24
-    d = (1 << L) >> 3
-    cP, cQ, cP2, cP3 = (oracle.splitmix64_np(s, d).astype(np.uint32) for s in (2001, 2002, 2003, 2004))
-    bad = cQ.copy()
-    bad[d // 2] = fri_amd.P
-    dQ, dbad, dP3 = _dev(torch, cQ), _dev(torch, bad), _dev(torch, cP3)
-    cx = fri_amd.Context(0, L)
+    d = (1 << log_n) >> 3
+    seeds_dev, seeds_host, seeds_buf = [1301, 1302], [1303, 1304], [1305, 1306, 1307]
+    devs = {s: _dev(torch, oracle.splitmix64_np(s, d).astype(np.uint32)) for s in seeds_dev}
+    host = {s: oracle.splitmix64_np(s, d).astype(np.uint32) for s in seeds_host}
+    cx = fri_amd.Context(0, log_n)
     try:
-        cx.set_lanes(2)
-        cx.commit(cP, L)                                                # the input buffer holds P
-        p0 = ctypes.c_void_p()
-        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p0)))
-        tA = cx.commit_device_async(dbad.data_ptr(), d, L)              # slot 0: lane 0, stages bad, stops early
-        tB = cx.commit_device_async(dQ.data_ptr(), d, L)                # slot 1: lane 1, a whole commit
-        tC = cx.commit_device_async(dbad.data_ptr(), d, L)              # slot 2: lane 0, stages bad, stops early
-        tD = cx.commit_device_async(p0.value, d, L)                     # slot 3: lane 1, reads the buffer
-        assert [cx.ticket_lane(t) for t in (tA, tB, tC, tD)] == [0, 1, 0, 1]
-        for t in (tA, tC):
-            with pytest.raises(fri_amd.FriError) as e:
-                cx.commit_wait(t)
-            assert e.value.code == fri_amd.FRI_EINVAL
-        sync = cx.commit(cP2, L)                                        # lane 0: stages P2
-        with pytest.raises(fri_amd.FriError) as e:
-            cx.commit_wait(tD)
-        assert e.value.code == fri_amd.FRI_EINVAL, "D did not read the buffer in call order"
-        resB = _transcript(cx.commit_wait(tB))
-        # a valid staging just before D
-        tA = cx.commit_device_async(dP3.data_ptr(), d, L)               # slot 0: lane 0, stages P3
-        tB2 = cx.commit_device_async(dQ.data_ptr(), d, L)               # lane 1
-        tD = cx.commit_device_async(p0.value, d, L)                     # slot 2: lane 0 (reads it directly)
-        tE = cx.commit_device_async(p0.value, d, L)                     # slot 3: lane 1, copy on lane 0's stream
-        assert [cx.ticket_lane(t) for t in (tA, tB2, tD, tE)] == [0, 1, 0, 1]
-        cx.commit(cP2, L)                                               # stages P2 after all of them
-        res = [_transcript(cx.commit_wait(t)) for t in (tA, tB2, tD, tE)]
+        cx.set_lanes(lanes)
+        p0 = cx.input_upload(oracle.splitmix64_np(seeds_buf[0], d).astype(np.uint32))
+        in_buf = seeds_buf[0]
+        pend, checked, uploads = [], 0, 0
+        rng = np.random.default_rng(log_n * 10 + lanes)
+        for i in range(40):
+            if len(pend) == fri_amd.MAX_INFLIGHT:
+                s0, t0 = pend.pop(0)
+                assert _transcript(cx.commit_wait(t0)) == oracle_commit(log_n, s0), (i, s0)
+                checked += 1
+            k = i % 5 if i < 20 else int(rng.integers(0, 5))
+            if k in (0, 3):                                          # the caller's buffer, read in place
+                pend.append((in_buf, cx.commit_device_async(p0, d, log_n)))
+            elif k == 1:                                             # another device buffer
+                s = seeds_dev[i % 2]
+                pend.append((s, cx.commit_device_async(devs[s].data_ptr(), d, log_n)))
+            elif k == 2:                                             # host coefficients
+                s = seeds_host[i % 2]
+                pend.append((s, cx.commit_async(host[s], log_n)))
+            else:                                                    # new contents, while commits of the old pend
+                in_buf = seeds_buf[(seeds_buf.index(in_buf) + 1) % len(seeds_buf)]
+                assert cx.input_upload(oracle.splitmix64_np(in_buf, d).astype(np.uint32)) == p0
+                uploads += 1
+        for s0, t0 in pend:
+            assert _transcript(cx.commit_wait(t0)) == oracle_commit(log_n, s0), s0
+            checked += 1
+        assert uploads >= 4 and checked >= 20 and checked + uploads == 40
+        # a synchronous commit from the buffer, and one from the host: neither changes it
+        assert _transcript(cx.commit(host[seeds_host[0]], log_n)) == oracle_commit(log_n, seeds_host[0])
+        res = fri_amd.CommitResult()
+        cx._check(cx.lib.fri_commit_device(cx.h, p0, d, log_n, fri_amd.GENERATOR, None, 0, None, ctypes.byref(res)))
+        assert _transcript(res) == oracle_commit(log_n, in_buf)
     finally:
         cx.close()
-    assert resB == oracle_commit(L, 2002)
-    assert _transcript(sync) == oracle_commit(L, 2003)
-    assert res == [oracle_commit(L, 2004), oracle_commit(L, 2002), oracle_commit(L, 2004), oracle_commit(L, 2004)]
+
+
+def test_input_buffer_grows_and_keeps_contents(oracle, oracle_commit):
+    """fri_ctx_input_buffer with a larger d moves the buffer (contents kept);
+    commits from the new pointer re-capture their graphs, and no commit needs
+    a plan before the buffer exists."""
+    import fri_amd
+    cx = fri_amd.Context(0, 18)
+    try:
+        d14, d16 = (1 << 14) >> 3, (1 << 16) >> 3
+        c14 = oracle.splitmix64_np(1401, d14).astype(np.uint32)
+        p14 = cx.input_upload(c14)                                   # before any commit on the context
+        res = fri_amd.CommitResult()
+        cx._check(cx.lib.fri_commit_device(cx.h, p14, d14, 14, fri_amd.GENERATOR, None, 0, None, ctypes.byref(res)))
+        assert _transcript(res) == oracle_commit(14, 1401)
+        p16 = cx.input_buffer(d16)                                   # larger: moved, first d14 words kept
+        cx._check(cx.lib.fri_commit_device(cx.h, p16, d14, 14, fri_amd.GENERATOR, None, 0, None, ctypes.byref(res)))
+        assert _transcript(res) == oracle_commit(14, 1401)
+        cx.input_upload(oracle.splitmix64_np(1601, d16).astype(np.uint32))
+        t = cx.commit_device_async(p16, d16, 16)
+        assert _transcript(cx.commit_wait(t)) == oracle_commit(16, 1601)
+        assert cx.input_buffer(d14) == p16                           # smaller: the same buffer
+        with pytest.raises(fri_amd.FriError) as e:
+            cx.input_buffer((1 << 18) + 1)                           # beyond the context's codeword bound
+        assert e.value.code == fri_amd.FRI_EINVAL
+    finally:
+        cx.close()
 
 
 def test_lanes_balanced_at_depth_four(pctx, oracle, oracle_commit, torch):
@@ -492,9 +511,9 @@ def test_rejected_sync_commit_keeps_pending_lane_commit_resident(pctx, oracle, o
 def test_lane_without_memory_falls_back_and_keeps_input_buffer(oracle, oracle_commit, torch):
     """A lane that gets no HBM for its plan (a device-memory cap on the
     context) drops out of the rotation: the commits run on lane 0, lane 0's
-    plan and the input buffer fri_ctx_input_buffer handed out stay valid (only
-    the partial plan is released), and every transcript is right.  Lifting the
-    cap and setting the lanes again brings the lanes back."""
+    plan and the input buffer stay valid (only the partial plan is released),
+    and every transcript is right.  Lifting the cap and setting the lanes
+    again brings the lanes back."""
     import fri_amd
     d = (1 << LOG_N) >> 3
     c0 = oracle.splitmix64_np(1201, d).astype(np.uint32)
@@ -502,8 +521,7 @@ def test_lane_without_memory_falls_back_and_keeps_input_buffer(oracle, oracle_co
     cx = fri_amd.Context(0, LOG_N)
     try:
         cx.commit(c0, LOG_N)
-        p0 = ctypes.c_void_p()
-        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p0)))
+        p0 = cx.input_upload(c0)
         cur = cx.device_bytes()[0]
         cx.set_device_cap(cur + (1 << 16))                   # lane state yes, a second plan no
         cx.set_lanes(3)
@@ -511,11 +529,8 @@ def test_lane_without_memory_falls_back_and_keeps_input_buffer(oracle, oracle_co
         assert [cx.ticket_lane(t) for _, t in ts] == [0, 0, 0]
         for s, t in ts:
             assert _transcript(cx.commit_wait(t)) == oracle_commit(LOG_N, s)
-        p1 = ctypes.c_void_p()
-        cx._check(cx.lib.fri_ctx_input_buffer(cx.h, d, ctypes.byref(p1)))
-        assert p1.value == p0.value
-        cx.commit(c0, LOG_N)                                  # the input buffer holds c0 again
-        t = cx.commit_device_async(p0.value, d, LOG_N)
+        assert cx.input_buffer(d) == p0
+        t = cx.commit_device_async(p0, d, LOG_N)             # the buffer still holds c0
         assert _transcript(cx.commit_wait(t)) == oracle_commit(LOG_N, 1201)
         cx.set_device_cap(0)
         cx.set_lanes(3)

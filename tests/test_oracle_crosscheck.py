@@ -227,3 +227,17 @@ def test_golden_decommit_reproduces(oracle, golden):
         assert len(ch.proof) - n0 == want["messages"]
         got = hashlib.sha256(b"".join(len(m).to_bytes(4, "little") + m for m in ch.proof[n0:])).hexdigest()
         assert got == want["proof_sha256"], c["name"]
+
+
+def test_flat_transcript_helper_matches_python_twin(oracle, corc):
+    """tests/oracle_flat.py (the C oracle's layers and trees, decommitted by
+    the Python twin through index views) gives the Python twin's own whole
+    transcript: commit messages, two queries' openings and the final state."""
+    import oracle_flat
+    for log_n, seed, state in ((9, 3, ""), (10, 4, "ab" * 32)):
+        coeffs = oracle.splitmix64_field(seed, (1 << log_n) // 8)
+        msgs, st = oracle_flat.transcript(corc, coeffs, log_n, 2, state=state)
+        ch = oracle.Channel(state=state)
+        r = oracle.fri_commit(coeffs, log_n, ch)
+        oracle.decommit_fri(2, (1 << log_n) - 1, r.layers, r.trees, ch)
+        assert msgs == ch.proof and st == ch.state

@@ -199,13 +199,15 @@ def test_team_rank_failure_does_not_block(team4, oracle, oracle_commit, rank, op
 
 def test_team_commit_device_from_rank0_buffer(team4, oracle, oracle_commit):
     """fri_commit_device on the team: the context's input buffer (rank 0's
-    device) is read by rank 0 in place and copied by the other ranks."""
+    device) is copied by rank 0 locally and by the other ranks over the
+    transport.  FRI_FLAG_RANK_INPUTS then reuses the ranks' staged copies,
+    verified against rank 0's buffer by a per-rank checksum: a buffer
+    rewritten since the staging gives FRI_ESTATE on every rank and commits
+    nothing, until a commit without the flag stages it again."""
     import fri_amd
     L = 22
     cf = _coeffs(oracle, 42, L)
-    team4.commit(cf, L)
-    p = ctypes.c_void_p()
-    team4._check(team4.lib.fri_ctx_input_buffer(team4.h, cf.size, ctypes.byref(p)))
+    p = ctypes.c_void_p(team4.input_upload(cf))
     out = fri_amd.CommitResult()
     for _ in range(3):
         team4._check(team4.lib.fri_commit_device(team4.h, p, cf.size, L, fri_amd.GENERATOR, None, 0, None,
@@ -216,11 +218,35 @@ def test_team_commit_device_from_rank0_buffer(team4, oracle, oracle_commit):
         team4._check(team4.lib.fri_commit_device(team4.h, p, cf.size, L, fri_amd.GENERATOR, None,
                                                  fri_amd.FLAG_RANK_INPUTS, None, ctypes.byref(out)))
         assert _transcript(out) == oracle_commit(L, 42)
-    # ... which a rank without an input buffer of this shape cannot do
+    # ... which needs rank 0's buffer and a staged copy of this shape
     for bad in ((p, cf.size // 2), (ctypes.c_void_p(p.value + 64), cf.size)):
         rc = team4.lib.fri_commit_device(team4.h, bad[0], bad[1], L, fri_amd.GENERATOR, None,
                                          fri_amd.FLAG_RANK_INPUTS, None, ctypes.byref(out))
         assert rc == fri_amd.FRI_ESTATE
+    # rank 0's buffer rewritten with same-shape coefficients: refused, nothing committed
+    g0 = team4.commit_info()[0]
+    cf2 = _coeffs(oracle, 43, L)
+    assert team4.input_upload(cf2) == p.value
+    rc = team4.lib.fri_commit_device(team4.h, p, cf.size, L, fri_amd.GENERATOR, None, fri_amd.FLAG_RANK_INPUTS,
+                                     None, ctypes.byref(out))
+    assert rc == fri_amd.FRI_ESTATE, rc
+    assert "differs from rank 0" in team4.lib.fri_last_error(team4.h).decode()
+    assert team4.commit_info()[0] == g0                   # the resident commit is untouched
+    assert np.array_equal(team4.layer(0, L), team4.lde(cf, L))
+    # one word changed is enough
+    cf3 = cf2.copy()
+    cf3[cf3.size // 3] ^= 1
+    team4._check(team4.lib.fri_commit_device(team4.h, p, cf.size, L, fri_amd.GENERATOR, None, 0, None,
+                                             ctypes.byref(out)))                  # stages cf2
+    assert _transcript(out) == oracle_commit(L, 43)
+    team4.input_upload(cf3)
+    rc = team4.lib.fri_commit_device(team4.h, p, cf.size, L, fri_amd.GENERATOR, None, fri_amd.FLAG_RANK_INPUTS,
+                                     None, ctypes.byref(out))
+    assert rc == fri_amd.FRI_ESTATE
+    team4.input_upload(cf2)
+    team4._check(team4.lib.fri_commit_device(team4.h, p, cf.size, L, fri_amd.GENERATOR, None,
+                                             fri_amd.FLAG_RANK_INPUTS, None, ctypes.byref(out)))
+    assert _transcript(out) == oracle_commit(L, 43)
 
 
 def test_team_create_arguments():
@@ -236,10 +262,73 @@ def test_team_create_arguments():
         assert c.dist_info()[2] == "none"
     finally:
         c.close()
+    c = fri_amd.Context.multi([0, 0], 21)                     # the default transport is the peer transport
+    try:
+        assert c.dist_info() == (0, 2, "peer")
+    finally:
+        c.close()
+
+
+def test_default_context_follows_fri_devices(monkeypatch, oracle, oracle_commit):
+    """fri_ctx_create_default (what the reference-signature bindings open):
+    FRI_DEVICES names the ranks ("0,0" -> a two-rank team on GPU 0), unset it
+    is every visible GPU (one here: an ordinary context); a malformed value is
+    FRI_EINVAL.  The Python mirror's fri_commit without ctx uses it."""
+    import fri_amd
+    monkeypatch.setenv("FRI_DEVICES", "0,0")
+    c = fri_amd.Context.default(21)
+    try:
+        assert c.n_ranks == 2 and c.dist_info() == (0, 2, "peer")
+        assert _transcript(c.commit(_coeffs(oracle, 6, 21), 21)) == oracle_commit(21, 6)
+    finally:
+        c.close()
+    for bad in ("0,0,0", "x", "0,,0"):
+        monkeypatch.setenv("FRI_DEVICES", bad)
+        with pytest.raises(fri_amd.FriError) as e:
+            fri_amd.Context.default(20)
+        assert e.value.code == fri_amd.FRI_EINVAL
+    monkeypatch.setenv("FRI_DEVICES", "0,0")
+    monkeypatch.setenv("FRI_TRANSPORT", "carrier-pigeon")
+    with pytest.raises(fri_amd.FriError):
+        fri_amd.Context.default(20)
+    monkeypatch.delenv("FRI_TRANSPORT")
+    monkeypatch.delenv("FRI_DEVICES")
+    c = fri_amd.Context.default(16)
+    try:
+        assert c.n_ranks >= 1 and c.dist_info()[2] == "none"
+    finally:
+        c.close()
+
+
+def test_reference_decommit_signature_on_team(team4, oracle):
+    """decommit_fri(num_queries, max_index, &fri_layers, &fri_merkles,
+    &mut channel) (fri_commit.rs:168-174), Python mirror, on a team commit:
+    the same messages as the proof form; layers of another commit and a stale
+    proof are refused."""
+    import fri_amd
+    L = 21
+    coeffs = _coeffs(oracle, 31, L)
+    ch_a = fri_amd.Channel()
+    proof = fri_amd.fri_commit(coeffs, L, ch_a, ctx=team4)
+    ch_b = fri_amd.Channel(state=ch_a.state, proof=list(ch_a.proof))
+    layers, merkles = proof.fri_layers, proof.fri_merkles
+    fri_amd.decommit_fri(2, (1 << L) - 1, layers, merkles, ch_a)
+    fri_amd.decommit_fri(2, (1 << L) - 1, proof, ch_b)
+    assert ch_a.proof == ch_b.proof and ch_a.state == ch_b.state
+    assert merkles[3].get_authentication_path(5) == b"".join(team4.auth_path(3, 5, L)[1])
+    wrong = [l.copy() for l in layers]
+    wrong[2] = (wrong[2] + 1) % fri_amd.P
+    with pytest.raises(fri_amd.FriError):
+        fri_amd.decommit_fri(3, (1 << L) - 1, wrong, merkles, fri_amd.Channel(state=ch_a.state))
+    fri_amd.fri_commit(_coeffs(oracle, 32, L), L, fri_amd.Channel(), ctx=team4)
+    with pytest.raises(fri_amd.FriError) as e:
+        fri_amd.decommit_fri(1, (1 << L) - 1, layers, merkles, fri_amd.Channel(state=ch_a.state))
+    assert e.value.code == fri_amd.FRI_ESTATE
 
 
 @pytest.mark.timeout(1200)
-def test_team_2p28_world8_configs4(oracle_commit):
+@pytest.mark.parametrize("copy", [False, True], ids=["pull", "copy"])
+def test_team_2p28_world8_configs4(oracle_commit, copy):
     """BASELINE configs[4]: the 2^28 codeword committed coset-sharded over 8
     ranks by ONE fri_commit call on a team context (peer transport, every
     rank on GPU 0: 8 shard-sized plans, ~50 GB), bit-exact against the C
@@ -250,6 +339,7 @@ def test_team_2p28_world8_configs4(oracle_commit):
     cf = fo.splitmix64_np(42, (1 << L) >> 3).astype(np.uint32)
     cx = fri_amd.Context.multi([0] * 8, L, transport="peer")
     try:
+        cx.force_copy(copy)          # copy: hipMemcpyPeerAsync per source (the no-peer-access path)
         res = cx.commit(cf, L)
         want = oracle_commit(L, 42)
         assert _transcript(res) == want
@@ -269,8 +359,9 @@ def test_team_2p28_world8_configs4(oracle_commit):
 _TF = int(os.environ.get("TEAM_FUZZ_N", "0"))      # > 0: that many cases per team size (longer runs)
 
 
+@pytest.mark.parametrize("copy", [False, True], ids=["pull", "copy"])
 @pytest.mark.parametrize("G,n_cases", [(2, _TF or 8), (4, _TF or 8), (8, _TF or 6)])
-def test_team_fuzz_vs_c_oracle(G, n_cases, corc, oracle):
+def test_team_fuzz_vs_c_oracle(G, n_cases, corc, oracle, copy):
     """Randomised team commits (the sharded fuzz's cases, dist_worker.fuzz_case:
     2^20..2^22, ragged coefficient counts including 0, blowups 1..16, degrees
     that end inside the sharded layers, zero / constant / odd-only polynomials,
@@ -278,13 +369,16 @@ def test_team_fuzz_vs_c_oracle(G, n_cases, corc, oracle):
     team of G ranks on GPU 0 (peer transport), one fri_commit call each:
     the whole transcript equals the OpenMP C oracle's 1-node commit
     (orc_fri_commit_fast, src/fri/fri_commit.rs:72-122), and the ranks'
-    transport logs pass the cross-rank schedule check."""
+    transport logs pass the cross-rank schedule check.  Run twice: over the pull
+kernel and over the hipMemcpyPeerAsync fallback a team takes where peer
+access is unavailable (fri_debug_team_force_copy)."""
     import fri_amd
     from dist_worker import fuzz_case, fuzz_forced_betas
     from test_dist import check_transport_schedule
-    seed = 1000 * G + 7
+    seed = 1000 * G + 7 + (500 if copy else 0)
     cx = fri_amd.Context.multi([0] * G, 22, transport="peer")
     try:
+        cx.force_copy(copy)
         for i in range(n_cases):
             log_n, c, offset, state = fuzz_case(seed + i, G)
             fb = fuzz_forced_betas(seed + i)

@@ -4,14 +4,15 @@ Thousands of commits on one or more fri_ctx driven from ONE host thread,
 each drawn at random from: synchronous commits from host coefficients or from
 a device buffer, pipelined commits of device buffers, of host coefficients
 (fri_commit_async; every context's uploads share the device's upload stream)
-and of the context's own input buffer (fri_ctx_input_buffer), with the number
-of commit lanes and the codeword shape of a context changing now and then.
-Every result is compared with the C oracle's transcript of the same
-polynomial (oracle/fri_oracle.c, the restatement of
-src/fri/fri_commit.rs:72-122), so an ordering race between lanes, stagings,
-result slots or contexts shows up as a wrong transcript.  A context's input
-buffer follows call order: a commit handed that buffer commits what the last
-synchronous commit or lane-0 staging of that context put there.
+and of the context's own input buffer (fri_ctx_input_buffer, refilled now and
+then with fri_ctx_input_upload), with the number of commit lanes and the
+codeword shape of a context changing now and then.  Every result is compared
+with the C oracle's transcript of the same polynomial (oracle/fri_oracle.c,
+the restatement of src/fri/fri_commit.rs:72-122), so an ordering race between
+lanes, stagings, result slots or contexts shows up as a wrong transcript.  The
+model of a context's input buffer needs nothing from the library: the buffer
+is the caller's, so it holds what the last upload put there, whatever the
+commits in between and however they were dealt to lanes.
 
     python3 tools/soak.py [--commits N] [--seed S] [--contexts K]
 """
@@ -49,8 +50,8 @@ def transcript(r):
 class Driven:
     """One context and the model of its state: the result slot of every
     pending ticket (lowest free slot, fri_lanes.hip async_enqueue), its lanes,
-    its shape and what its input buffer holds in call order (a pipelined
-    commit dealt to lane 0 stages its coefficients there)."""
+    its shape and what its input buffer holds (the last upload's
+    polynomial)."""
 
     def __init__(self, fri_amd, polys, rng):
         self.fa, self.polys, self.rng = fri_amd, polys, rng
@@ -83,7 +84,6 @@ class Driven:
         if u < 0.02:                               # another shape: every lane's plan is rebuilt
             self.drain()
             self.L = int(rng.choice(SHAPES))
-            self.in_buf = None
         elif u < 0.04:                             # another number of lanes (no commit may be pending)
             self.drain()
             self.lanes = int(rng.integers(1, fa.MAX_INFLIGHT + 1))
@@ -91,35 +91,36 @@ class Driven:
         L = self.L
         d = (1 << L) >> 3
         j = int(rng.integers(0, 4))
-        kind = int(rng.integers(0, 5))
-        if kind == 4 and self.in_buf is None:
-            kind = 0
+        kind = int(rng.integers(0, 6))
+        if kind == 4 and (self.in_buf is None or self.in_buf[0] != L):
+            kind = 5                               # the buffer holds no polynomial of this shape yet
         if len(self.pend) == fa.MAX_INFLIGHT:
             self.expect_oldest()
         c, dev, want = self.polys[(L, j)]
-        if kind == 0:                              # synchronous, host coefficients: staged (lane 0)
+        if kind == 0:                              # synchronous, host coefficients (staged privately)
             assert transcript(ctx.commit(c, L)) == want
             self.n_ok += 1
-            self.in_buf = (L, j)
-        elif kind == 1:                            # synchronous, device buffer: staged into the input buffer
+        elif kind == 1:                            # synchronous, another device buffer (staged privately)
             r = fa.CommitResult()
             ctx._check(ctx.lib.fri_commit_device(ctx.h, ctypes.c_void_p(dev.data_ptr()), d, L, fa.GENERATOR,
                                                  None, 0, None, ctypes.byref(r)))
             assert transcript(r) == want
             self.n_ok += 1
-            self.in_buf = (L, j)
         elif kind in (2, 3):                       # pipelined, device buffer / host coefficients
             t = ctx.commit_device_async(dev.data_ptr(), d, L) if kind == 2 else ctx.commit_async(c, L)
             self.enqueue(t, (L, j))
-            # a commit dealt to lane 0 stages its input into the input buffer
-            # (the deal itself, fewest pending first, is the library's:
-            # fri_debug_ticket_lane reports it)
-            if ctx.ticket_lane(t) == 0:
-                self.in_buf = (L, j)
-        else:                                      # pipelined, the context's own input buffer
-            p0 = ctypes.c_void_p()
-            ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(p0)))
-            self.enqueue(ctx.commit_device_async(p0.value, d, L), self.in_buf)
+        elif kind == 4:                            # pipelined, the context's own input buffer, read in place
+            self.enqueue(ctx.commit_device_async(ctx.input_buffer(d), d, L), self.in_buf)
+        else:                                      # refill the input buffer (waits for its pending readers)
+            ctx.input_upload(c)
+            self.in_buf = (L, j)
+            # ... and, half the time, commit it at once (synchronously)
+            if rng.random() < 0.5:
+                r = fa.CommitResult()
+                ctx._check(ctx.lib.fri_commit_device(ctx.h, ctypes.c_void_p(ctx.input_buffer(d)), d, L,
+                                                     fa.GENERATOR, None, 0, None, ctypes.byref(r)))
+                assert transcript(r) == want
+                self.n_ok += 1
         kinds[kind] = kinds.get(kind, 0) + 1
 
 
@@ -153,7 +154,7 @@ def main(argv=None):
     n_ok = sum(c.n_ok for c in cx)
     print(f"soak ok: {n_ok} commits on {len(cx)} context(s) checked against the C oracle in {time.time() - t0:.1f} s "
           f"(kinds: sync-host {kinds.get(0, 0)}, sync-device {kinds.get(1, 0)}, async-device {kinds.get(2, 0)}, "
-          f"async-host {kinds.get(3, 0)}, async-input-buffer {kinds.get(4, 0)})", flush=True)
+          f"async-host {kinds.get(3, 0)}, async-input-buffer {kinds.get(4, 0)}, upload {kinds.get(5, 0)})", flush=True)
     return n_ok, kinds
 
 
