@@ -295,6 +295,10 @@ def main():
         # A job spread over several nodes keeps RCCL's own interface choice.
         if int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world:
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        # a rendezvous or collective that makes no progress ends in FRI_ERCCL
+        # after this many seconds (fri_amd.h; library default 120): the
+        # fallbacks after a failed RCCL run then still fit a bench run's budget
+        os.environ.setdefault("FRI_RCCL_TIMEOUT_S", "60")
         import torch
         import torch.distributed as dist
         ndev = torch.cuda.device_count()          # does not initialise HIP
