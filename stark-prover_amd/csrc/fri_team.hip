@@ -303,7 +303,9 @@ static int default_devices(std::vector<int>& dev, int& transport) {
         size_t i = 0;
         while (i <= v.size()) {
             const size_t j = std::min(v.find(',', i), v.size());
-            const std::string tok = v.substr(i, j - i);
+            std::string tok = v.substr(i, j - i);
+            while (!tok.empty() && tok.front() == ' ') tok.erase(tok.begin());     // "0, 1" as well as "0,1"
+            while (!tok.empty() && tok.back() == ' ') tok.pop_back();
             if (tok.empty() || tok.size() > 4 || tok.find_first_not_of("0123456789") != std::string::npos)
                 return FRI_EINVAL;
             dev.push_back(atoi(tok.c_str()));
