@@ -25,8 +25,7 @@ for c in range(C):
     ctx = fri_amd.Context(0, log_n)
     co = _coeffs(42 + c, d, fri_amd.P)
     want.append(ctx.commit(co, log_n))
-    p = ctypes.c_void_p()
-    ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(p)))
+    p = ctypes.c_void_p(ctx.input_upload(co))
     ctxs.append(ctx); ptrs.append(p); res.append(fri_amd.CommitResult())
 
 

@@ -16,8 +16,7 @@ ref = ctxs[0].commit(c, log_n)
 dptr = {}
 for x in ctxs:
     x.commit(c, log_n)
-    p = ctypes.c_void_p()
-    x._check(x.lib.fri_ctx_input_buffer(x.h, d, ctypes.byref(p)))
+    p = ctypes.c_void_p(x.input_upload(c))
     dptr[id(x)] = p
 for K, dev in ((1, False), (2, False), (3, False), (4, False), (1, True), (2, True), (3, True), (4, True)):
     cx = ctxs[:K]

@@ -11,8 +11,7 @@ log_n = 24; d = 1 << 21
 ctx = fri_amd.Context(0, log_n)
 c = _coeffs(42, d, fri_amd.P)
 ctx.commit(c, log_n)
-dptr = ctypes.c_void_p()
-ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(dptr)))
+dptr = ctypes.c_void_p(ctx.input_upload(c))
 for kind in ("device", "host", "host", "device"):
     enq, wt = [], []
     pend = []

@@ -59,8 +59,7 @@ def run(log_n, world, rank, steps, serial_coef=False):
     print(f"rank {rank}/{world}, 2^{log_n}: {r.n_layers} layers, {r.n_rounds} rounds; "
           f"{steps + 1} loopback commits in {time.perf_counter() - t0:.4f} s", flush=True)
     # timed as bench.py times the sharded step: coefficients resident in HBM
-    dptr = ctypes.c_void_p()
-    ctx._check(ctx.lib.fri_ctx_input_buffer(ctx.h, d, ctypes.byref(dptr)))
+    dptr = ctypes.c_void_p(ctx.input_upload(coeffs))     # the context's input buffer, filled once
     res = fri_amd.CommitResult()
     t0 = time.perf_counter()
     for _ in range(steps):
