@@ -87,6 +87,7 @@ struct Plan {
     const uint32_t* graph_src[FRI_MAX_INFLIGHT + 1][2] = {};
     hipGraph_t tail_graph = nullptr;        // sharded plan: the local layers after the switch
     hipGraphExec_t tail_exec = nullptr;
+    const uint32_t* tail_src = nullptr;     // the input pointer tail_exec was captured with
     bool graph_profiled = false;
 };
 

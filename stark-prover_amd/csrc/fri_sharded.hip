@@ -37,14 +37,19 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
     ctx->sharded_layers = (uint32_t)p.rmax + 1;      // lowered when the tail goes local
     init_state(ctx, ctx->h_sync, chan_in, flags, forced_betas);
     FRI_HIP(ctx, hipMemcpyAsync(ctx->d_state, ctx->h_state, sizeof(DevState), hipMemcpyHostToDevice, s));
-    // the input is always staged into the plan's own buffer (rank 0 of a team
-    // copies the caller's buffer locally, ranks 1..G-1 over xGMI), so the
-    // launches below and the local tail's graph read one fixed pointer
-    if (host_coeffs && d)
-        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
-    else if (dev_coeffs && dev_coeffs != p.d_in && d)   // (Default: a team rank reads rank 0's device buffer)
-        FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDefault, s));
-    p.src = p.d_in;
+    // the input: this context's own input buffer (fri_ctx_input_buffer) is
+    // read in place, anything else is staged into the plan's private buffer
+    // (a team rank copies rank 0's buffer over xGMI; FRI_FLAG_RANK_INPUTS
+    // hands it the copy staged there before)
+    if (dev_coeffs && d && ctx->user_in && dev_coeffs == ctx->user_in) {
+        p.src = ctx->user_in;
+    } else {
+        if (host_coeffs && d)
+            FRI_HIP(ctx, hipMemcpyAsync(p.d_in, host_coeffs, d * 4, hipMemcpyHostToDevice, s));
+        else if (dev_coeffs && dev_coeffs != p.d_in && d)   // (Default: a team rank reads rank 0's device buffer)
+            FRI_HIP(ctx, hipMemcpyAsync(p.d_in, dev_coeffs, d * 4, hipMemcpyDefault, s));
+        p.src = p.d_in;
+    }
 
     size_t sp;
     if (G == 2) {
@@ -301,6 +306,14 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
         if (ctx->profiling || (flags & FRI_FLAG_NO_GRAPH)) {
             if ((rc = local_tail())) return rc;
         } else {
+            // (a tail that begins at layer 1 folds the input itself: its
+            // graph names the input pointer, captured again when it changes)
+            if (p.tail_exec && p.tail_src != p.src) {
+                hipGraphExecDestroy(p.tail_exec);
+                hipGraphDestroy(p.tail_graph);
+                p.tail_exec = nullptr;
+                p.tail_graph = nullptr;
+            }
             if (!p.tail_exec) {
                 FRI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
                 rc = local_tail();
@@ -313,6 +326,7 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
                 }
                 p.tail_graph = g;
                 FRI_HIP(ctx, hipGraphInstantiate(&p.tail_exec, g, nullptr, nullptr, 0));
+                p.tail_src = p.src;
             }
             FRI_HIP(ctx, hipGraphLaunch(p.tail_exec, s));
         }

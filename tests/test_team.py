@@ -250,6 +250,27 @@ def test_team_commit_device_from_rank0_buffer(team4, oracle, oracle_commit):
     assert _transcript(out) == oracle_commit(L, 43)
 
 
+def test_team_input_in_place_and_tail_graph(team4, oracle, oracle_commit):
+    """At 2^20 over 4 ranks the sharded part is layer 0 alone, so the local
+    tail (one hipGraph per plan) folds the input coefficients itself: its
+    graph names the input pointer.  Commits alternating between host input
+    (staged in the plan's buffer) and rank 0's input buffer (read in place)
+    re-capture it; every transcript equals the C oracle's."""
+    import fri_amd
+    L = 20
+    cf, cg = _coeffs(oracle, 61, L), _coeffs(oracle, 62, L)
+    p = ctypes.c_void_p(team4.input_upload(cg))
+    out = fri_amd.CommitResult()
+    for _ in range(2):
+        assert _transcript(team4.commit(cf, L)) == oracle_commit(L, 61)
+        team4._check(team4.lib.fri_commit_device(team4.h, p, cg.size, L, fri_amd.GENERATOR, None, 0, None,
+                                                 ctypes.byref(out)))
+        assert _transcript(out) == oracle_commit(L, 62)
+    team4._check(team4.lib.fri_commit_device(team4.h, p, cg.size, L, fri_amd.GENERATOR, None,
+                                             fri_amd.FLAG_RANK_INPUTS, None, ctypes.byref(out)))
+    assert _transcript(out) == oracle_commit(L, 62)
+
+
 def test_team_create_arguments():
     import fri_amd
     with pytest.raises(fri_amd.FriError):
