@@ -58,7 +58,7 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
         // both size-M NTTs on every rank, then this rank's block.
         sp = span_begin(ctx, "lde", d * 4 + M * 12);
         const size_t de = (d + 1) / 2, dod = d / 2;
-        launch_decimate(p.d_in, d, ctx->scratch_a, ctx->scratch_b, s);
+        launch_decimate(p.src, d, ctx->scratch_a, ctx->scratch_b, s);
         launch_pow_table(db.pre_lo, db.pre_hi, log_n - 1, mul_std(offset, offset), 1u, s);
         NttPlan np{};
         np.log_n = log_n - 1;
@@ -77,14 +77,14 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
         // P mod (x^M - s^M) has P's own coefficients when d <= M (blowup >= G):
         // the NTT then reads the input directly (and skips its zero rows)
         const bool fold_chunks = d > M;
-        if (fold_chunks) launch_coset_coeffs(p.d_in, d, db.recv, M, pow_std(sft, M), s);
+        if (fold_chunks) launch_coset_coeffs(p.src, d, db.recv, M, pow_std(sft, M), s);
         launch_pow_table(db.pre_lo, db.pre_hi, log_n - logG, sft, 1u, s);
         NttPlan np{};
         np.log_n = log_n - logG;
         np.tw = ctx->tw_fwd;
         np.pre_lo = db.pre_lo;
         np.pre_hi = db.pre_hi;
-        launch_ntt(np, fold_chunks ? db.recv : p.d_in, fold_chunks ? M : d, db.cyc, s);
+        launch_ntt(np, fold_chunks ? db.recv : p.src, fold_chunks ? M : d, db.cyc, s);
         span_end(ctx, sp);
         sp = span_begin(ctx, "alltoall", M * 4);
         rc = tp_alltoall(ctx, db.cyc, db.recv, (M / G) * 4, s);                       // coset slices -> blocks
@@ -109,7 +109,7 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
             ShardTop& t = sh[kk];
             t.rec_out = db.rec;
             t.rec_mx = p.wgmax;
-            t.rec_c0 = kk ? coef_buf(p, kk) : p.d_in;
+            t.rec_c0 = kk ? coef_buf(p, kk) : p.src;
             t.rec_R = coef_grid(kk);
             t.G = G;
             t.recs_in = db.rec + REC_WORDS;
@@ -118,7 +118,8 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
             for (uint32_t b2 = 0; b2 < G; b2++) t.rank_of_block[b2] = (uint8_t)ro[b2];
             advance_blocks(bo, ro, G);
         }
-        // the table depends only on the plan (and the loopback schedule), so
+        // the table depends only on the plan, the input pointer and the
+        // loopback schedule, so
         // it is uploaded when it changes, from a copy that outlives the call:
         // no host sync in front of the commit's first launch.  The previous
         // sharded call ended with a stream sync, so its upload has completed.
@@ -201,7 +202,7 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
         const size_t Sk = (size_t)1 << (p.cs0 - (uint32_t)k);
         LayerTask tc{};
         tc.k = k;
-        tc.coef_in = (k <= 1) ? p.d_in : coef_buf(p, k - 1);
+        tc.coef_in = (k <= 1) ? p.src : coef_buf(p, k - 1);
         tc.ibase = (k <= 1) ? 0 : (size_t)rank * (Sk << 1);
         tc.coef_out = k ? coef_buf(p, k) : nullptr;
         tc.obase = (size_t)rank * Sk;
