@@ -119,9 +119,9 @@ int fri::run_commit_sharded(fri_ctx* ctx, const uint32_t* host_coeffs, const uin
             advance_blocks(bo, ro, G);
         }
         // the table depends only on the plan, the input pointer and the
-        // loopback schedule, so
-        // it is uploaded when it changes, from a copy that outlives the call:
-        // no host sync in front of the commit's first launch.  The previous
+        // loopback schedule, so it is uploaded when it changes, from a copy
+        // that outlives the call: no host sync in front of the commit's first
+        // launch.  The previous
         // sharded call ended with a stream sync, so its upload has completed.
         if (db.shtop_h.size() != sh.size() || memcmp(db.shtop_h.data(), sh.data(), sh.size() * sizeof(ShardTop))) {
             db.shtop_h = sh;
