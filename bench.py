@@ -70,15 +70,20 @@ def valu_issue_units(log_n, d):
     return leaves * LEAF_ISSUE_UNITS + nodes * NODE_ISSUE_UNITS
 
 
-def whole_commit_valu(log_n, d, ms_per_commit):
-    """valu_issue_units over the time of one commit, against the nominal
-    VALU peak and the measured issue ceiling (the chain's idle chip shows here,
-    where the dominant kernel's own roofline cannot see it)."""
+def whole_commit_valu(log_n, d, ms_per_commit, n_commits=1, n_dev=1):
+    """valu_issue_units of n_commits commits over ms_per_commit on n_dev GPUs,
+    against the nominal VALU peak and the measured issue ceiling of those GPUs
+    (the chain's idle chip shows here, where the dominant kernel's own
+    roofline cannot see it)."""
     units = valu_issue_units(log_n, d)
-    t = units / (ms_per_commit * 1e-3) / 1e12
-    return {"issue_units_per_commit": units, "ms_per_commit": round(ms_per_commit, 4), "achieved": round(t, 2),
-            "unit": "T int32 lane-ops/s", "peak": VALU_PEAK_TOPS, "frac": round(t / VALU_PEAK_TOPS, 4),
-            "measured_ceiling": VALU_MEASURED_TOPS, "frac_of_measured_ceiling": round(t / VALU_MEASURED_TOPS, 4)}
+    t = n_commits * units / (ms_per_commit * 1e-3) / 1e12
+    out = {"issue_units_per_commit": units, "ms_per_commit": round(ms_per_commit, 4), "achieved": round(t, 2),
+           "unit": "T int32 lane-ops/s", "peak": VALU_PEAK_TOPS * n_dev, "frac": round(t / (VALU_PEAK_TOPS * n_dev), 4),
+           "measured_ceiling": VALU_MEASURED_TOPS * n_dev,
+           "frac_of_measured_ceiling": round(t / (VALU_MEASURED_TOPS * n_dev), 4)}
+    if n_commits != 1 or n_dev != 1:
+        out.update(commits=n_commits, n_gpus=n_dev)
+    return out
 
 
 def sha_compressions(log_n, d):
@@ -650,12 +655,11 @@ def main():
     # every layer over ms_per_step -- what the serial Fiat-Shamir chain costs
     # shows here, not in the dominant kernel's roofline -- and the same work
     # over the pipelined per-commit time (commit lanes fill the idle chip)
-    n_dev_valu = (1 << logG) if mode == "sharded" else 1
-    whole["valu"] = whole_commit_valu(log_n, d, ms_per_step)
-    if n_dev_valu > 1:
-        whole["valu"]["n_gpus"] = n_dev_valu
-        whole["valu"]["frac"] = round(whole["valu"]["frac"] / n_dev_valu, 4)
-        whole["valu"]["frac_of_measured_ceiling"] = round(whole["valu"]["frac_of_measured_ceiling"] / n_dev_valu, 4)
+    # (on the distinct GPUs the work ran on; replicas: one commit per rank)
+    n_ranks_all = (dist_report or {}).get("world_reported", world) if mode == "sharded" else world
+    n_dev, oversub = devices_used(team_devices if team_n else None, world, ndev_all, n_ranks_all)
+    whole["valu"] = whole_commit_valu(log_n, d, ms_per_step, n_commits=world if mode == "replicas" else 1,
+                                      n_dev=n_dev)
     if pipelined and pipelined.get("ms_per_commit"):
         whole["valu_pipelined"] = dict(whole_commit_valu(log_n, d, pipelined["ms_per_commit"]),
                                        lanes=pipelined.get("best_lanes"),
@@ -737,13 +741,12 @@ def main():
         configs0 = _configs0_stage(ctx)
 
     if rank == 0:
-        # the sharded run's size as its communicator (or the team) reports it
-        n_ranks = (dist_report or {}).get("world_reported", world) if mode == "sharded" else world
-        # GPUs the job actually ran on: fewer than the ranks when ranks share
-        # a device (a rehearsal on a box with fewer GPUs than --gpus); such a
-        # run reports n_gpus = the distinct devices and keeps its points out
-        # of scaling_points
-        n_dev, oversub = devices_used(team_devices if team_n else None, world, ndev_all, n_ranks)
+        # the sharded run's size as its communicator (or the team) reports it;
+        # n_dev: the GPUs the job actually ran on, fewer than the ranks when
+        # ranks share a device (a rehearsal on a box with fewer GPUs than
+        # --gpus): such a run reports n_gpus = the distinct devices and keeps
+        # its points out of scaling_points
+        n_ranks = n_ranks_all
         if mode == "sharded":
             workload = (f"fri_commit codeword 2^{log_n}, blowup {1 << args.blowup_log} (d=2^{log_n - args.blowup_log}), "
                         f"coset-sharded over {n_ranks} {'GPUs' if not oversub else f'ranks on {n_dev} GPU(s)'} "

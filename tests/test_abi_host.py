@@ -143,6 +143,11 @@ def test_bench_whole_commit_valu_arithmetic():
     assert abs(v["frac"] - 0.518) < 0.002 and abs(v["frac_of_measured_ceiling"] - 0.636) < 0.002
     assert abs(bench.whole_commit_valu(24, 1 << 21, 3.3138)["frac"] - 0.7215) < 0.002
     assert bench.valu_issue_units(10, 1) == 1024 * 2009.0 + 1023 * 3592.0   # degree 0: one layer
+    # over several GPUs (sharded: one commit on n_dev devices; replicas: one commit per rank)
+    two = bench.whole_commit_valu(24, 1 << 21, 4.613, n_commits=1, n_dev=2)
+    assert abs(two["frac"] - v["frac"] / 2) < 1e-3 and two["n_gpus"] == 2 and two["peak"] == 2 * 78.6
+    rep = bench.whole_commit_valu(24, 1 << 21, 4.613, n_commits=2, n_dev=2)
+    assert abs(rep["frac"] - v["frac"]) < 1e-3 and abs(rep["achieved"] - 2 * v["achieved"]) < 0.05
 
 
 # ---- verify_fri (host mirror) on oracle-produced transcripts -------------
