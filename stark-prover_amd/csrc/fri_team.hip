@@ -134,17 +134,17 @@ static std::map<std::pair<int, int>, PeerRef> g_peer;
 
 static bool peer_acquire(int a, int b) {
     std::lock_guard<std::mutex> g(g_peer_m);
-    PeerRef& pr = g_peer[{a, b}];
-    if (pr.refs == 0) {
+    auto it = g_peer.find({a, b});
+    if (it == g_peer.end()) {
         int can = 0;
         if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) return false;
         (void)hipSetDevice(a);
         const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
         (void)hipGetLastError();
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return false;
-        pr.ours = e == hipSuccess;
+        it = g_peer.emplace(std::make_pair(a, b), PeerRef{0, e == hipSuccess}).first;
     }
-    pr.refs++;
+    it->second.refs++;
     return true;
 }
 
