@@ -143,7 +143,22 @@ assert lib.fri_ctx_destroy(None) == 1
 tr = (ctypes.c_uint32 * 1024)()
 assert lib.fri_fibsq_trace(3141592, 10, tr) == 0 and tr[0] == 1 and tr[1] == 3141592
 assert lib.fri_fibsq_trace(P, 10, tr) != 0
-print(json.dumps({"layouts": n, "ctx_rc": rc_ctx}))
+# the default-device parser (fri_ctx_create_default): malformed FRI_DEVICES /
+# FRI_TRANSPORT are FRI_EINVAL before any device is touched
+import os
+nr = ctypes.c_uint32()
+bad = 0
+for dv, tp in (("0,0,0", ""), ("x", ""), ("0,,0", ""), ("0" * 9, ""), (",".join(["0"] * 128), ""), ("0,0", "smoke")):
+    os.environ["FRI_DEVICES"] = dv
+    os.environ["FRI_TRANSPORT"] = tp
+    bad += lib.fri_ctx_create_default(20, ctypes.byref(h), ctypes.byref(nr)) == 1
+os.environ["FRI_DEVICES"] = " 0 , 0 "
+os.environ["FRI_TRANSPORT"] = "peer"
+rc_def = lib.fri_ctx_create_default(20, ctypes.byref(h), ctypes.byref(nr))
+assert nr.value == 2 and rc_def in (0, 4), (rc_def, nr.value)
+if rc_def == 0:
+    lib.fri_ctx_destroy(h)
+print(json.dumps({"layouts": n, "ctx_rc": rc_ctx, "default_einval": bad}))
 """
 
 
@@ -160,3 +175,4 @@ def test_library_host_code_under_asan_ubsan():
                  {"LD_PRELOAD": rt, "ASAN_OPTIONS": "detect_leaks=0:halt_on_error=1",
                   "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"})
     assert out["layouts"] > 2000
+    assert out["default_einval"] == 6

@@ -282,6 +282,9 @@ def test_team_create_arguments():
     c = fri_amd.Context.multi([0], 16)                        # one device: an ordinary context
     try:
         assert c.dist_info()[2] == "none"
+        with pytest.raises(fri_amd.FriError) as e:
+            c.force_copy(True)                                # a test hook of teams only
+        assert e.value.code == fri_amd.FRI_EINVAL
     finally:
         c.close()
     c = fri_amd.Context.multi([0, 0], 21)                     # the default transport is the peer transport
