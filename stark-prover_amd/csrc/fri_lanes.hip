@@ -280,13 +280,13 @@ extern "C" int fri_ctx_input_upload(fri_ctx* ctx, const uint32_t* coeffs, size_t
     if (!d) return FRI_OK;
     FRI_HIP(ctx, hipSetDevice(ctx->device));
     if ((rc = wait_user_readers(ctx))) return rc;
-    // no pending commit reads the buffer now (synchronous commits have
-    // returned): the copy goes on the device's upload stream, not behind
-    // the unrelated commits queued on the lanes (nor on the null stream,
-    // which would hold a hardware queue of its own)
-    if (!ctx->h2d_stream) FRI_HIP(ctx, upload_stream(ctx->device, &ctx->h2d_stream));
-    FRI_HIP(ctx, hipMemcpyAsync(buf, coeffs, d * 4, hipMemcpyHostToDevice, ctx->h2d_stream));
-    FRI_HIP(ctx, hipStreamSynchronize(ctx->h2d_stream));
+    // on the context stream, ordered after every commit queued there.  Not
+    // on the upload stream: creating it here would hold a hardware queue
+    // from the first upload on, and three commit lanes plus the context
+    // stream plus that one exceed GPU_MAX_HW_QUEUES (4), which serialised
+    // the 3-lane pipelined commits (4.09 against 3.30 ms per 2^24 commit)
+    FRI_HIP(ctx, hipMemcpyAsync(buf, coeffs, d * 4, hipMemcpyHostToDevice, ctx->stream));
+    FRI_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return FRI_OK;
 }
 
