@@ -1153,9 +1153,13 @@ def _prover_stage(ctx, fri_amd, with_cpu, log_t=16, log_b=3, queries=3, a1=31415
     # loop), when stark-prover_amd/build/prover_native is built
     exe = os.path.join(ROOT, "stark-prover_amd", "build", "prover_native")
     if os.path.exists(exe):
+        # its Gpu::thread_default would open every visible GPU
+        # (fri_ctx_create_default): pin it to this rank's device
+        env = dict(os.environ, FRI_DEVICES=str(ctx_device(ctx)))
+        env.pop("FRI_TRANSPORT", None)
         try:
             r = subprocess.run([exe, str(log_t), str(log_b), str(queries), "10"], capture_output=True, text=True,
-                               timeout=120)
+                               timeout=120, env=env)
             out["native_cpp"] = json.loads(r.stdout.strip().splitlines()[-1])
         except Exception as e:  # noqa: BLE001
             out["native_cpp"] = {"error": str(e)}
